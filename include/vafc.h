@@ -1,0 +1,182 @@
+/*
+ * vafc.h -- C ABI of the MI355X-native vaf-counter hot path (libvafc.so).
+ *
+ * The reference (gerbenvoshol/kmer-cnt, vaf-counter.c) is a monolithic C
+ * program with no plugin/FFI API; its in-process seam is
+ *
+ *     void count_fastq_kmers(const char *fn, int k, int n_thread, int block_size,
+ *                            kmer_cnt_t *kmer_map, pattern_db_t *db);   // vaf-counter.c:550
+ *
+ * fed by load_patterns() (vaf-counter.c:149) and create_combined_kmer_map()
+ * (vaf-counter.c:198), with steps 1+2 of its pipeline (extract k-mers
+ * vaf-counter.c:519-535, look up + increment vaf-counter.c:537-544) as the hot
+ * path.  This header is that seam re-cut at a device boundary: plain pointers
+ * and sizes, no torch or HIP types, C linkage.  Every entry point names the
+ * reference interface it replaces.
+ *
+ * Counts layout: uint32 counts[2*n_patterns], REF of pattern i at [2i], ALT at
+ * [2i+1] -- i.e. indexed by the reference's map value (i<<1)|is_alt
+ * (vaf-counter.c:227,239).  Counts wrap modulo 2^32 exactly like the
+ * reference's uint32 fields (vaf-counter.c:101-102,473-477).
+ *
+ * Errors: 0 = ok, <0 = VC_E* below; vc_strerror() gives text.  HIP failures
+ * are reported, never silently degraded to a CPU path.
+ */
+#ifndef VAFC_H
+#define VAFC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VAFC_VERSION_MAJOR 0
+#define VAFC_VERSION_MINOR 1
+
+enum {
+	VC_OK = 0,
+	VC_EINVAL = -1,      /* bad argument (k outside 1..31, NULL pointer, ...) */
+	VC_ENOMEM = -2,      /* host allocation failed */
+	VC_EHIP = -3,        /* HIP runtime / kernel launch error */
+	VC_ENODEV = -4,      /* no usable GPU */
+	VC_EIO = -5,         /* file could not be opened / read */
+	VC_ETOOMANY = -6     /* more than INT32_MAX>>1 patterns (vaf-counter.c:205-209) */
+};
+
+typedef struct vc_ctx vc_ctx;
+typedef struct vc_patterns vc_patterns;
+
+/* ------------------------------------------------------------------ */
+/* Pattern database -- replaces load_patterns (vaf-counter.c:149-184)  */
+/* and create_combined_kmer_map (vaf-counter.c:198-252).               */
+/* ------------------------------------------------------------------ */
+
+/* Load patterns.txt (records "chr start end rsid ref alt ref_kmer alt_kmer",
+ * read with the reference's fscanf conversion; reading stops at the first
+ * record that does not convert completely).  Returns VC_EIO if the file
+ * cannot be opened (the reference then exits 1, vaf-counter.c:624-627). */
+int vc_patterns_load(const char *path, vc_patterns **out);
+void vc_patterns_free(vc_patterns *db);
+int vc_patterns_count(const vc_patterns *db);
+
+/* Canonical 2-bit keys and values (i<<1)|is_alt in insertion order (ref of
+ * pattern i, then alt of pattern i), first insert wins, keys of strings with a
+ * non-ACGTU character among their first k skipped.  *keys / *vals are malloc'd
+ * (caller frees with vc_free).  *n_collisions = duplicate inserts ignored. */
+int vc_patterns_keys(const vc_patterns *db, int k, uint64_t **keys, uint32_t **vals,
+                     size_t *n_keys, int *n_collisions);
+
+/* Write the .vaf file (vaf-counter.c:653-681): header "# Average depth",
+ * column line, one row per pattern in file order. counts as above. */
+int vc_write_vaf(const vc_patterns *db, const uint32_t *counts, const char *path);
+
+/* Field access for host-side mirrors (Python): returns 0 and fills the
+ * pointers (valid until vc_patterns_free). */
+int vc_pattern_fields(const vc_patterns *db, int i, const char **chr, int *start,
+                      const char **rsid, char *ref, char *alt,
+                      const char **ref_kmer, const char **alt_kmer);
+
+void vc_free(void *p);
+
+/* ------------------------------------------------------------------ */
+/* Device counter -- replaces the kmer_cnt_t map + pattern_t counters  */
+/* (vaf-counter.c:67,92-108) and steps 1+2 of worker_pipeline          */
+/* (vaf-counter.c:519-544, worker_lookup :449-479).                    */
+/* ------------------------------------------------------------------ */
+
+/* Create a counter on HIP device `device` for k in 1..31 from (key, value)
+ * pairs as produced by vc_patterns_keys (first occurrence of a key wins).
+ * The static key table and its LDS prefilter are built on the host and copied
+ * once to HBM.  Counts start at zero. */
+int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32_t *vals,
+              size_t n_keys, uint32_t n_patterns, int device);
+void vc_destroy(vc_ctx *ctx);
+
+/* Count one block of host-resident reads (asynchronous; accumulates).
+ * seq: raw read bytes exactly as the FASTA/Q parser returned them (the
+ * position-dependent 2-bit decode of vaf-counter.c:261-291 is applied on the
+ * device); read i is seq[offs[i] .. offs[i]+lens[i]).  The caller may reuse
+ * its buffers as soon as the call returns (they are staged into pinned
+ * memory).  Reads shorter than k contribute nothing. */
+int vc_count_block(vc_ctx *ctx, const uint8_t *seq, size_t seq_bytes,
+                   const uint64_t *offs, const uint32_t *lens, uint64_t n_reads);
+
+/* Same for device-resident reads (HBM pointers, e.g. from torch or
+ * hipMalloc); enqueued on `stream` (a hipStream_t, NULL = the ctx stream).
+ * No host synchronisation.  seq_bytes bounds every device read. */
+int vc_count_device(vc_ctx *ctx, const uint8_t *d_seq, size_t seq_bytes,
+                    const uint64_t *d_offs, const uint32_t *d_lens, uint64_t n_reads,
+                    void *stream);
+
+/* Wait for all queued work; copy counts[2*n_patterns] and the number of valid
+ * k-mers extracted (perf_stats_t.total_kmers_extracted, vaf-counter.c:388)
+ * to the host.  Either output may be NULL. */
+int vc_finish(vc_ctx *ctx, uint32_t *counts, uint64_t *kmers_extracted);
+
+/* Zero counts and the k-mer tally (asynchronous on the ctx stream). */
+int vc_reset(vc_ctx *ctx);
+
+/* Device pointer of the uint32 counts[2*n_patterns] array (for a device-side
+ * all-reduce across ranks, e.g. RCCL through torch.distributed). */
+void *vc_device_counts(vc_ctx *ctx);
+void *vc_device_tally(vc_ctx *ctx);
+void *vc_stream(vc_ctx *ctx);
+
+/* Kernel timing: when enabled, every count call records HIP events around
+ * the k-mer kernel on the stream it runs on; vc_kernel_ms synchronises on the
+ * last pair and returns its elapsed milliseconds (sum of both kernels). */
+int vc_set_timing(vc_ctx *ctx, int enable);
+int vc_kernel_ms(vc_ctx *ctx, float *ms);
+
+/* Table/prefilter geometry, for reports: n_keys, table slots, filter bytes. */
+int vc_table_info(const vc_ctx *ctx, uint64_t *n_keys, uint64_t *slots, uint64_t *filter_bytes);
+
+/* ------------------------------------------------------------------ */
+/* Whole-file pass -- replaces count_fastq_kmers (vaf-counter.c:550).  */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+	uint64_t bases;        /* bases of reads with len >= k (pipeline_t.total_bases) */
+	uint64_t seqs;         /* reads with len >= k (pipeline_t.total_seqs) */
+	uint64_t blocks;       /* non-empty -b blocks */
+	double seconds;        /* wall time of this file */
+} vc_file_stats;
+
+/* Parse FASTA/FASTQ (plain or gzip) with kseq_read semantics (kseq.h:192-232)
+ * under the reference's block loop: blocks of >= block_bases bases, reads
+ * shorter than k skipped, a read error (-2) or EOF ends a block, the file ends
+ * at the third empty block (vaf-counter.c:486-517, kthread.c:97-128).  Reads
+ * are streamed to the device in large pinned batches.  n_threads is accepted
+ * for CLI parity (-t).  Returns VC_EIO if the file cannot be opened (the
+ * reference skips such files silently, vaf-counter.c:557). */
+int vc_count_file(vc_ctx *ctx, const char *path, int block_bases, int n_threads,
+                  vc_file_stats *st);
+
+/* ------------------------------------------------------------------ */
+/* Synthetic workload (bench / tests): the generator of vafc_synth.py,  */
+/* evaluated on the device.                                            */
+/* ------------------------------------------------------------------ */
+
+/* Generate reads first..first+n_reads-1 (fixed length read_len) into device
+ * buffers d_seq[n_reads*read_len], d_offs[n_reads], d_lens[n_reads].
+ * d_windows: device [n_snp][2][301] ASCII SNP windows, d_dosage: [n_snp] u8. */
+int vc_synth_reads(uint8_t *d_seq, uint64_t *d_offs, uint32_t *d_lens, uint64_t first,
+                   uint64_t n_reads, uint32_t read_len, uint64_t seed, double f_snp,
+                   const uint8_t *d_windows, const uint8_t *d_dosage, uint32_t n_snp,
+                   void *stream);
+
+/* Test hook: position-dependent 2-bit decode (vaf-counter.c:261-291) of
+ * device-resident reads into d_codes (same offsets as d_seq; 0..3, 4 =
+ * invalid) by the kernels' own decode path. */
+int vc_debug_decode(const uint8_t *d_seq, size_t seq_bytes, const uint64_t *d_offs,
+                    const uint32_t *d_lens, uint64_t n_reads, uint8_t *d_codes, void *stream);
+
+const char *vc_strerror(int err);
+int vc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,123 @@
+// vafc_fastq.cpp -- see vafc_fastq.h.
+#include "vafc_fastq.h"
+
+#include <ctype.h>
+#include <stdlib.h>
+
+bool VcFastqReader::open(const char *path, size_t window)
+{
+	close();
+	fp_ = gzopen(path, "r");
+	if (!fp_) return false;
+	gzbuffer(fp_, 1u << 20);
+	cap_ = window;
+	buf_ = (uint8_t *)malloc(cap_);
+	b_ = e_ = 0;
+	eof_ = false;
+	hdr_ = 0;
+	return buf_ != nullptr;
+}
+
+void VcFastqReader::close()
+{
+	if (fp_) gzclose(fp_);
+	fp_ = nullptr;
+	free(buf_);
+	buf_ = nullptr;
+}
+
+bool VcFastqReader::refill()
+{
+	if (eof_) return false;
+	int n = gzread(fp_, buf_, (unsigned)cap_);
+	if (n <= 0) {
+		eof_ = true;
+		b_ = e_ = 0;
+		return false;
+	}
+	b_ = 0;
+	e_ = (size_t)n;
+	return true;
+}
+
+// Bytes up to the next '\n' (consumed, not stored) appended to dst; -1 only
+// if the input was exhausted on entry (kseq.h:106).  Afterwards a trailing
+// '\r' of the whole accumulated string is dropped when it is longer than one
+// byte (kseq.h:146).
+int VcFastqReader::line(VcByteBuf *dst)
+{
+	if (at_end()) return -1;
+	for (;;) {
+		const uint8_t *p = buf_ + b_;
+		const size_t n = e_ - b_;
+		const uint8_t *nl = (const uint8_t *)memchr(p, '\n', n);
+		if (nl) {
+			dst->append(p, (size_t)(nl - p));
+			b_ += (size_t)(nl - p) + 1;
+			break;
+		}
+		dst->append(p, n);
+		b_ = e_;
+		if (!refill()) break;
+	}
+	if (dst->l > 1 && dst->s[dst->l - 1] == '\r') --dst->l;
+	return (int)dst->l;
+}
+
+// Name token: up to an isspace() byte (KS_SEP_SPACE); the delimiter (or 0 at
+// end of input) is returned through delim.
+int VcFastqReader::token(int *delim)
+{
+	*delim = 0;
+	if (at_end()) return -1;
+	for (;;) {
+		while (b_ < e_) {
+			int c = buf_[b_++];
+			if (isspace(c)) {
+				*delim = c;
+				return 0;
+			}
+		}
+		if (!refill()) return 0;
+	}
+}
+
+void VcFastqReader::skip_line()
+{
+	for (;;) {
+		const uint8_t *p = buf_ + b_;
+		const uint8_t *nl = (const uint8_t *)memchr(p, '\n', e_ - b_);
+		if (nl) {
+			b_ += (size_t)(nl - p) + 1;
+			return;
+		}
+		b_ = e_;
+		if (!refill()) return;
+	}
+}
+
+int VcFastqReader::next()
+{
+	int c, d;
+	if (!hdr_) { // scan to a '>' or '@' (kseq.h:197-201)
+		do c = getc_(); while (c != -1 && c != '>' && c != '@');
+		if (c == -1) return -1;
+		hdr_ = c;
+	}
+	seq_.l = qual_.l = 0;
+	if (token(&d) < 0) return -1;
+	if (d != '\n' && !at_end()) skip_line();          // comment (kseq.h:204)
+	// sequence lines until a line starts with '+', '>' or '@' (kseq.h:209-213)
+	while ((c = getc_()) != -1 && c != '>' && c != '+' && c != '@') {
+		if (c == '\n') continue;
+		seq_.push(c);
+		line(&seq_);
+	}
+	if (c == '>' || c == '@') hdr_ = c;
+	if (c != '+') return (int)seq_.l;                 // FASTA
+	do c = getc_(); while (c != -1 && c != '\n');     // rest of the '+' line
+	if (c == -1) return -2;
+	while (line(&qual_) >= 0 && qual_.l < seq_.l) {}
+	hdr_ = 0;
+	return seq_.l == qual_.l ? (int)seq_.l : -2;
+}

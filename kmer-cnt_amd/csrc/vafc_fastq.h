@@ -1,0 +1,70 @@
+// vafc_fastq.h -- FASTA/FASTQ record reader with the reference's kseq_read
+// semantics (kseq.h:101-149 ks_getuntil2, kseq.h:192-232 kseq_read), written
+// for throughput: a large refillable window, memchr line scans, the sequence
+// and quality of a record kept in reusable buffers.  zlib's gzread reads both
+// plain and gzip input (vaf-counter.c:12,557).
+//
+// Return values of next(): >= 0 sequence length, -1 end of input, -2
+// truncated or length-mismatched quality -- exactly kseq_read's.
+#ifndef VAFC_FASTQ_H
+#define VAFC_FASTQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+
+class VcByteBuf {
+public:
+	char *s = nullptr;
+	size_t l = 0, m = 0;
+	~VcByteBuf() { free(s); }
+	void reserve(size_t n)
+	{
+		if (n <= m) return;
+		size_t nm = m ? m : 256;
+		while (nm < n) nm *= 2;
+		s = (char *)realloc(s, nm);
+		m = nm;
+	}
+	void push(int c) { reserve(l + 1); s[l++] = (char)c; }
+	void append(const uint8_t *p, size_t n)
+	{
+		reserve(l + n);
+		memcpy(s + l, p, n);
+		l += n;
+	}
+};
+
+class VcFastqReader {
+public:
+	VcFastqReader() = default;
+	~VcFastqReader() { close(); }
+	bool open(const char *path, size_t window = (size_t)4 << 20);
+	void close();
+	int next();
+	const char *seq() const { return seq_.s; }
+	size_t seq_len() const { return seq_.l; }
+
+private:
+	gzFile fp_ = nullptr;
+	uint8_t *buf_ = nullptr;
+	size_t cap_ = 0, b_ = 0, e_ = 0;
+	bool eof_ = false;
+	int hdr_ = 0;                 // header char already consumed, 0 if none
+	VcByteBuf seq_, qual_;
+
+	bool refill();
+	inline int getc_()
+	{
+		if (b_ >= e_ && !refill()) return -1;
+		return buf_[b_++];
+	}
+	inline bool at_end() { return b_ >= e_ && !refill(); }
+	int line(VcByteBuf *dst);     // rest of a line, appended; CR rule on the whole string
+	int token(int *delim);        // up to an isspace() byte, discarded
+	void skip_line();
+};
+
+#endif

@@ -1,0 +1,700 @@
+// vafc_host.cpp -- host side of libvafc.so: the C ABI of include/vafc.h.
+//
+//   patterns      load_patterns / create_combined_kmer_map   vaf-counter.c:149-252
+//   device ctx    static key table + LDS prefilter in HBM, counts, streams
+//   count_block   host block -> pinned staging -> H2D -> kernels (async)
+//   count_file    count_fastq_kmers: block loop + kseq reader  vaf-counter.c:482-582
+//   write_vaf     .vaf writer                                  vaf-counter.c:653-681
+//
+// Nothing here computes counts on the CPU: every k-mer goes through the HIP
+// kernels in vafc_kernels.hip, and any HIP failure is returned as VC_EHIP.
+#include <hip/hip_runtime.h>
+
+#include <limits.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <unordered_map>
+#include <vector>
+
+#include "vafc.h"
+#include "vafc_common.h"
+#include "vafc_fastq.h"
+#include "vafc_internal.h"
+
+#define HIPCK(call)                                                                         \
+	do {                                                                                    \
+		hipError_t e_ = (call);                                                             \
+		if (e_ != hipSuccess) {                                                             \
+			fprintf(stderr, "[E::vafc] %s failed: %s (%s:%d)\n", #call, hipGetErrorString(e_), \
+			        __FILE__, __LINE__);                                                    \
+			return VC_EHIP;                                                                 \
+		}                                                                                   \
+	} while (0)
+
+// ---------------------------------------------------------------------------
+// patterns
+// ---------------------------------------------------------------------------
+
+namespace {
+
+struct Pattern {
+	char chr[256];
+	int start, end;
+	char rsid[256];
+	char ref, alt;
+	char ref_kmer[128];
+	char alt_kmer[128];
+};
+
+unsigned char g_nt4[256];
+bool g_nt4_init = false;
+
+void init_nt4()
+{
+	if (g_nt4_init) return;
+	for (int i = 0; i < 256; ++i) g_nt4[i] = 4;
+	for (int i = 0; i < 4; ++i) g_nt4[i] = (unsigned char)i;
+	const char *acgt[4] = {"Aa", "Cc", "Gg", "TtUu"};
+	for (int c = 0; c < 4; ++c)
+		for (const char *p = acgt[c]; *p; ++p) g_nt4[(unsigned char)*p] = (unsigned char)c;
+	g_nt4_init = true;
+}
+
+// 2-bit key of the first k characters (vaf-counter.c:117-127); UINT64_MAX if
+// any of them is not A/C/G/T/U (either case) or a raw byte 0..3.
+uint64_t string_key(const char *s, int k)
+{
+	uint64_t x = 0;
+	for (int i = 0; i < k; ++i) {
+		unsigned c = g_nt4[(unsigned char)s[i]];
+		if (c > 3) return UINT64_MAX;
+		x = (x << 2) | c;
+	}
+	return x;
+}
+
+uint64_t canonical(uint64_t x, int k)
+{
+	uint64_t r = 0, y = x;
+	for (int i = 0; i < k; ++i, y >>= 2) r = (r << 2) | (3u - (y & 3u));
+	return r < x ? r : x;
+}
+
+} // namespace
+
+struct vc_patterns {
+	std::vector<Pattern> a;
+};
+
+extern "C" int vc_patterns_load(const char *path, vc_patterns **out)
+{
+	if (!path || !out) return VC_EINVAL;
+	*out = nullptr;
+	FILE *fp = fopen(path, "r");
+	if (!fp) return VC_EIO;
+	vc_patterns *db = new (std::nothrow) vc_patterns;
+	if (!db) {
+		fclose(fp);
+		return VC_ENOMEM;
+	}
+	// One record buffer reused across records, like the reference's local
+	// pattern_t: a k-mer string shorter than k is followed by its NUL and by
+	// bytes of earlier longer strings (the reference's buffer starts as
+	// uninitialised stack; this one starts zeroed).
+	Pattern rec;
+	memset(&rec, 0, sizeof(rec));
+	while (fscanf(fp, "%255s%d%d%255s %c %c%127s%127s", rec.chr, &rec.start, &rec.end, rec.rsid,
+	              &rec.ref, &rec.alt, rec.ref_kmer, rec.alt_kmer) == 8)
+		db->a.push_back(rec);
+	fclose(fp);
+	*out = db;
+	return VC_OK;
+}
+
+extern "C" void vc_patterns_free(vc_patterns *db) { delete db; }
+
+extern "C" int vc_patterns_count(const vc_patterns *db) { return db ? (int)db->a.size() : 0; }
+
+extern "C" int vc_pattern_fields(const vc_patterns *db, int i, const char **chr, int *start,
+                                 const char **rsid, char *ref, char *alt, const char **ref_kmer,
+                                 const char **alt_kmer)
+{
+	if (!db || i < 0 || (size_t)i >= db->a.size()) return VC_EINVAL;
+	const Pattern &p = db->a[(size_t)i];
+	if (chr) *chr = p.chr;
+	if (start) *start = p.start;
+	if (rsid) *rsid = p.rsid;
+	if (ref) *ref = p.ref;
+	if (alt) *alt = p.alt;
+	if (ref_kmer) *ref_kmer = p.ref_kmer;
+	if (alt_kmer) *alt_kmer = p.alt_kmer;
+	return VC_OK;
+}
+
+extern "C" void vc_free(void *p) { free(p); }
+
+extern "C" int vc_patterns_keys(const vc_patterns *db, int k, uint64_t **keys, uint32_t **vals,
+                                size_t *n_keys, int *n_collisions)
+{
+	if (!db || !keys || !vals || !n_keys || k < 1 || k > 31) return VC_EINVAL;
+	const size_t n = db->a.size();
+	if (n > (size_t)(INT32_MAX >> 1)) return VC_ETOOMANY;   // vaf-counter.c:205-209
+	init_nt4();
+	uint64_t *K = (uint64_t *)malloc((2 * n + 1) * sizeof(uint64_t));
+	uint32_t *V = (uint32_t *)malloc((2 * n + 1) * sizeof(uint32_t));
+	if (!K || !V) {
+		free(K);
+		free(V);
+		return VC_ENOMEM;
+	}
+	std::unordered_map<uint64_t, uint32_t> seen;
+	seen.reserve(2 * n + 1);
+	size_t m = 0;
+	int coll = 0;
+	for (size_t i = 0; i < n; ++i) {
+		for (int allele = 0; allele < 2; ++allele) {
+			const char *s = allele ? db->a[i].alt_kmer : db->a[i].ref_kmer;
+			uint64_t x = string_key(s, k);
+			if (x == UINT64_MAX) continue;
+			uint64_t c = canonical(x, k);
+			uint32_t v = ((uint32_t)i << 1) | (uint32_t)allele;
+			if (seen.emplace(c, v).second) {
+				K[m] = c;
+				V[m] = v;
+				++m;
+			} else {
+				++coll;                     // first insert wins (khashl.h:218)
+			}
+		}
+	}
+	*keys = K;
+	*vals = V;
+	*n_keys = m;
+	if (n_collisions) *n_collisions = coll;
+	return VC_OK;
+}
+
+extern "C" int vc_write_vaf(const vc_patterns *db, const uint32_t *counts, const char *path)
+{
+	if (!db || !path) return VC_EINVAL;
+	const size_t n = db->a.size();
+	uint64_t tot_ref = 0, tot_alt = 0;
+	for (size_t i = 0; i < n; ++i) {
+		tot_ref += counts ? counts[2 * i] : 0;
+		tot_alt += counts ? counts[2 * i + 1] : 0;
+	}
+	const double avg = (double)(tot_ref + tot_alt) / (n > 0 ? (double)n : 1.0);
+	FILE *fp = fopen(path, "w");
+	if (!fp) return VC_EIO;
+	setvbuf(fp, nullptr, _IOFBF, 1 << 20);
+	fprintf(fp, "# Average depth: %.2f\n", avg);
+	fprintf(fp, "CHR\tPOS\tRSID\tREF\tALT\tREF_COUNT\tALT_COUNT\tTOTAL_COUNT\tVAF\n");
+	for (size_t i = 0; i < n; ++i) {
+		const Pattern &p = db->a[i];
+		const uint32_t rc = counts ? counts[2 * i] : 0, ac = counts ? counts[2 * i + 1] : 0;
+		const uint32_t tot = rc + ac;                       // u32 wrap, as the reference
+		const double vaf = tot > 0 ? (double)ac / tot : 0.0;
+		fprintf(fp, "%s\t%d\t%s\t%c\t%c\t%u\t%u\t%u\t%.4f\n", p.chr, p.start, p.rsid, p.ref, p.alt, rc,
+		        ac, tot, vaf);
+	}
+	return fclose(fp) == 0 ? VC_OK : VC_EIO;
+}
+
+// ---------------------------------------------------------------------------
+// device context
+// ---------------------------------------------------------------------------
+
+namespace {
+
+struct Slot {
+	uint8_t *h_seq = nullptr;     // pinned
+	uint64_t *h_offs = nullptr;
+	uint32_t *h_lens = nullptr;
+	uint8_t *d_seq = nullptr;
+	uint64_t *d_offs = nullptr;
+	uint32_t *d_lens = nullptr;
+	size_t cap_bytes = 0, cap_reads = 0;
+	hipEvent_t done = nullptr;
+	bool pending = false;
+};
+
+} // namespace
+
+struct vc_ctx {
+	int dev = 0, k = 21;
+	uint32_t n_patterns = 0;
+	uint64_t n_keys = 0;
+	hipStream_t st = nullptr;
+	int n_cu = 256;
+	uint64_t *d_tkeys = nullptr;
+	uint32_t *d_tvals = nullptr;
+	uint32_t tbits = 0;
+	uint32_t *d_filter = nullptr;
+	uint32_t wbits = 0;
+	uint32_t *d_counts = nullptr;
+	unsigned long long *d_tally = nullptr;
+	uint32_t *d_nlong = nullptr;
+	uint32_t *d_long = nullptr;
+	uint32_t long_cap = 0;
+	Slot slot[2];
+	int cur = 0;
+	bool timing = false, timed = false;
+	hipEvent_t t0 = nullptr, t1 = nullptr;
+};
+
+static int ensure_long_cap(vc_ctx *c, uint64_t seq_bytes)
+{
+	uint64_t need = seq_bytes / (VC_LONG_READ + 1) + 1;
+	if (need <= c->long_cap) return VC_OK;
+	if (need > 0xFFFFFFFFull) need = 0xFFFFFFFFull;
+	HIPCK(hipStreamSynchronize(c->st));
+	if (c->d_long) HIPCK(hipFree(c->d_long));
+	c->d_long = nullptr;
+	HIPCK(hipMalloc(&c->d_long, need * sizeof(uint32_t)));
+	c->long_cap = (uint32_t)need;
+	return VC_OK;
+}
+
+extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32_t *vals,
+                         size_t n_keys, uint32_t n_patterns, int device)
+{
+	if (!out || k < 1 || k > 31 || (n_keys && (!keys || !vals))) return VC_EINVAL;
+	*out = nullptr;
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VC_ENODEV;
+	if (device < 0 || device >= ndev) return VC_EINVAL;
+	HIPCK(hipSetDevice(device));
+	HIPCK(vc_kernel_setup());
+
+	vc_ctx *c = new (std::nothrow) vc_ctx;
+	if (!c) return VC_ENOMEM;
+	c->dev = device;
+	c->k = k;
+	c->n_patterns = n_patterns;
+	hipDeviceProp_t prop;
+	if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+		c->n_cu = prop.multiProcessorCount;
+
+	// exact table: linear probing, load <= 1/2
+	uint32_t tbits = 4;
+	while (((uint64_t)1 << tbits) < 2 * (uint64_t)n_keys + 2) ++tbits;
+	const uint64_t tslots = (uint64_t)1 << tbits;
+	std::vector<uint64_t> tk(tslots, VC_EMPTY_KEY);
+	std::vector<uint32_t> tv(tslots, 0);
+	// prefilter: >= 24 bits per key, 1 KiB .. 128 KiB
+	uint32_t wbits = 8;
+	while (wbits < VC_MAX_FILTER_WBITS && ((uint64_t)32 << wbits) < 24 * (uint64_t)n_keys) ++wbits;
+	std::vector<uint32_t> fw((size_t)1 << wbits, 0);
+	uint64_t inserted = 0;
+	for (size_t i = 0; i < n_keys; ++i) {
+		const uint64_t key = keys[i];
+		if (key == VC_EMPTY_KEY) continue;
+		const uint32_t h = vc_hash(key);
+		uint32_t s = vc_table_slot(h, tbits);
+		bool dup = false;
+		while (tk[s] != VC_EMPTY_KEY) {
+			if (tk[s] == key) { dup = true; break; }
+			s = (s + 1) & (uint32_t)(tslots - 1);
+		}
+		if (dup) continue;             // first occurrence wins
+		tk[s] = key;
+		tv[s] = vals[i];
+		fw[vc_filter_word(h, wbits)] |= vc_filter_mask(h, wbits);
+		++inserted;
+	}
+	c->n_keys = inserted;
+	c->tbits = tbits;
+	c->wbits = wbits;
+
+	int rc = VC_OK;
+#define TRY(call)                                                                        \
+	do {                                                                                 \
+		hipError_t e_ = (call);                                                          \
+		if (e_ != hipSuccess) {                                                          \
+			fprintf(stderr, "[E::vafc] %s failed: %s\n", #call, hipGetErrorString(e_)); \
+			rc = VC_EHIP;                                                                \
+			goto fail;                                                                   \
+		}                                                                                \
+	} while (0)
+	TRY(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+	TRY(hipMalloc(&c->d_tkeys, tslots * sizeof(uint64_t)));
+	TRY(hipMalloc(&c->d_tvals, tslots * sizeof(uint32_t)));
+	TRY(hipMalloc(&c->d_filter, fw.size() * sizeof(uint32_t)));
+	TRY(hipMalloc(&c->d_counts, (2 * (size_t)n_patterns + 2) * sizeof(uint32_t)));
+	TRY(hipMalloc(&c->d_tally, sizeof(unsigned long long)));
+	TRY(hipMalloc(&c->d_nlong, sizeof(uint32_t)));
+	TRY(hipMemcpy(c->d_tkeys, tk.data(), tslots * sizeof(uint64_t), hipMemcpyHostToDevice));
+	TRY(hipMemcpy(c->d_tvals, tv.data(), tslots * sizeof(uint32_t), hipMemcpyHostToDevice));
+	TRY(hipMemcpy(c->d_filter, fw.data(), fw.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+	TRY(hipMemset(c->d_counts, 0, (2 * (size_t)n_patterns + 2) * sizeof(uint32_t)));
+	TRY(hipMemset(c->d_tally, 0, sizeof(unsigned long long)));
+	TRY(hipEventCreate(&c->t0));
+	TRY(hipEventCreate(&c->t1));
+	for (auto &s : c->slot) TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+	if ((rc = ensure_long_cap(c, (uint64_t)1 << 30)) != VC_OK) goto fail;
+#undef TRY
+	*out = c;
+	return VC_OK;
+fail:
+	vc_destroy(c);
+	return rc;
+}
+
+static void free_slot(Slot &s)
+{
+	if (s.h_seq) (void)hipHostFree(s.h_seq);
+	if (s.h_offs) (void)hipHostFree(s.h_offs);
+	if (s.h_lens) (void)hipHostFree(s.h_lens);
+	if (s.d_seq) (void)hipFree(s.d_seq);
+	if (s.d_offs) (void)hipFree(s.d_offs);
+	if (s.d_lens) (void)hipFree(s.d_lens);
+	s.h_seq = nullptr;
+	s.h_offs = nullptr;
+	s.h_lens = nullptr;
+	s.d_seq = nullptr;
+	s.d_offs = nullptr;
+	s.d_lens = nullptr;
+	s.cap_bytes = s.cap_reads = 0;
+	s.pending = false;
+}
+
+extern "C" void vc_destroy(vc_ctx *c)
+{
+	if (!c) return;
+	(void)hipSetDevice(c->dev);
+	if (c->st) (void)hipStreamSynchronize(c->st);
+	for (auto &s : c->slot) {
+		free_slot(s);
+		if (s.done) (void)hipEventDestroy(s.done);
+	}
+	if (c->t0) (void)hipEventDestroy(c->t0);
+	if (c->t1) (void)hipEventDestroy(c->t1);
+	if (c->d_tkeys) (void)hipFree(c->d_tkeys);
+	if (c->d_tvals) (void)hipFree(c->d_tvals);
+	if (c->d_filter) (void)hipFree(c->d_filter);
+	if (c->d_counts) (void)hipFree(c->d_counts);
+	if (c->d_tally) (void)hipFree(c->d_tally);
+	if (c->d_nlong) (void)hipFree(c->d_nlong);
+	if (c->d_long) (void)hipFree(c->d_long);
+	if (c->st) (void)hipStreamDestroy(c->st);
+	delete c;
+}
+
+// Enqueue the two counting kernels over device-resident reads on stream st.
+static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint64_t *d_offs,
+                  const uint32_t *d_lens, uint64_t n_reads, hipStream_t st)
+{
+	if (n_reads == 0) return VC_OK;
+	int rc = ensure_long_cap(c, seq_bytes);
+	if (rc != VC_OK) return rc;
+	VcKernelArgs A;
+	const uintptr_t p = (uintptr_t)d_seq;
+	A.seq = (const uint8_t *)(p & ~(uintptr_t)3);
+	A.off_adj = (uint64_t)(p & 3u);
+	A.seq_words = (seq_bytes + A.off_adj + 3) / 4;
+	A.offs = d_offs;
+	A.lens = d_lens;
+	A.n_reads = n_reads;
+	A.tkeys = c->d_tkeys;
+	A.tvals = c->d_tvals;
+	A.tbits = c->tbits;
+	A.tmask = (uint32_t)(((uint64_t)1 << c->tbits) - 1);
+	A.filter = c->d_filter;
+	A.wbits = c->wbits;
+	A.k = c->k;
+	A.kmask = ((uint64_t)1 << (2 * c->k)) - 1;
+	A.counts = c->d_counts;
+	A.tally = c->d_tally;
+	A.nlong = c->d_nlong;
+	A.longlist = c->d_long;
+	A.long_cap = c->long_cap;
+	uint64_t groups = (n_reads + VC_BLOCK - 1) / VC_BLOCK;
+	int grid = (int)(groups < (uint64_t)c->n_cu ? groups : (uint64_t)c->n_cu);
+	HIPCK(hipMemsetAsync(c->d_nlong, 0, sizeof(uint32_t), st));
+	if (c->timing) HIPCK(hipEventRecord(c->t0, st));
+	HIPCK(vc_launch_count(&A, grid, c->n_cu, st));
+	if (c->timing) {
+		HIPCK(hipEventRecord(c->t1, st));
+		c->timed = true;
+	}
+	return VC_OK;
+}
+
+extern "C" int vc_count_device(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes,
+                               const uint64_t *d_offs, const uint32_t *d_lens, uint64_t n_reads,
+                               void *stream)
+{
+	if (!c || (n_reads && (!d_seq || !d_offs || !d_lens))) return VC_EINVAL;
+	HIPCK(hipSetDevice(c->dev));
+	return launch(c, d_seq, seq_bytes, d_offs, d_lens, n_reads,
+	              stream ? (hipStream_t)stream : c->st);
+}
+
+static int slot_reserve(Slot &s, size_t bytes, size_t reads)
+{
+	if (bytes <= s.cap_bytes && reads <= s.cap_reads) return VC_OK;
+	if (s.pending) HIPCK(hipEventSynchronize(s.done));
+	s.pending = false;
+	size_t nb = s.cap_bytes > bytes ? s.cap_bytes : bytes + bytes / 4 + 4096;
+	size_t nr = s.cap_reads > reads ? s.cap_reads : reads + reads / 4 + 1024;
+	free_slot(s);
+	HIPCK(hipHostMalloc(&s.h_seq, nb, hipHostMallocDefault));
+	HIPCK(hipHostMalloc(&s.h_offs, nr * sizeof(uint64_t), hipHostMallocDefault));
+	HIPCK(hipHostMalloc(&s.h_lens, nr * sizeof(uint32_t), hipHostMallocDefault));
+	HIPCK(hipMalloc(&s.d_seq, nb));
+	HIPCK(hipMalloc(&s.d_offs, nr * sizeof(uint64_t)));
+	HIPCK(hipMalloc(&s.d_lens, nr * sizeof(uint32_t)));
+	s.cap_bytes = nb;
+	s.cap_reads = nr;
+	return VC_OK;
+}
+
+// Wait until a slot's previous batch has left its pinned buffers.
+static int slot_acquire(vc_ctx *c, Slot **out)
+{
+	Slot &s = c->slot[c->cur];
+	if (s.pending) {
+		HIPCK(hipEventSynchronize(s.done));
+		s.pending = false;
+	}
+	*out = &s;
+	return VC_OK;
+}
+
+// H2D copy of a filled slot + kernels; the slot is released by its event.
+static int slot_submit(vc_ctx *c, Slot &s, size_t bytes, uint64_t n_reads)
+{
+	if (n_reads) {
+		HIPCK(hipMemcpyAsync(s.d_seq, s.h_seq, bytes, hipMemcpyHostToDevice, c->st));
+		HIPCK(hipMemcpyAsync(s.d_offs, s.h_offs, n_reads * sizeof(uint64_t), hipMemcpyHostToDevice, c->st));
+		HIPCK(hipMemcpyAsync(s.d_lens, s.h_lens, n_reads * sizeof(uint32_t), hipMemcpyHostToDevice, c->st));
+		int rc = launch(c, s.d_seq, bytes, s.d_offs, s.d_lens, n_reads, c->st);
+		if (rc != VC_OK) return rc;
+		HIPCK(hipEventRecord(s.done, c->st));
+		s.pending = true;
+	}
+	c->cur ^= 1;
+	return VC_OK;
+}
+
+extern "C" int vc_count_block(vc_ctx *c, const uint8_t *seq, size_t seq_bytes, const uint64_t *offs,
+                              const uint32_t *lens, uint64_t n_reads)
+{
+	if (!c || (n_reads && (!seq || !offs || !lens))) return VC_EINVAL;
+	if (n_reads == 0) return VC_OK;
+	HIPCK(hipSetDevice(c->dev));
+	for (uint64_t i = 0; i < n_reads; ++i)
+		if (offs[i] + lens[i] > seq_bytes) return VC_EINVAL;
+	Slot *s;
+	int rc = slot_acquire(c, &s);
+	if (rc == VC_OK) rc = slot_reserve(*s, seq_bytes, n_reads);
+	if (rc != VC_OK) return rc;
+	memcpy(s->h_seq, seq, seq_bytes);
+	memcpy(s->h_offs, offs, n_reads * sizeof(uint64_t));
+	memcpy(s->h_lens, lens, n_reads * sizeof(uint32_t));
+	return slot_submit(c, *s, seq_bytes, n_reads);
+}
+
+extern "C" int vc_finish(vc_ctx *c, uint32_t *counts, uint64_t *kmers)
+{
+	if (!c) return VC_EINVAL;
+	HIPCK(hipSetDevice(c->dev));
+	HIPCK(hipStreamSynchronize(c->st));
+	HIPCK(hipDeviceSynchronize());
+	for (auto &s : c->slot) s.pending = false;
+	if (counts)
+		HIPCK(hipMemcpy(counts, c->d_counts, 2 * (size_t)c->n_patterns * sizeof(uint32_t),
+		                hipMemcpyDeviceToHost));
+	if (kmers) {
+		unsigned long long t = 0;
+		HIPCK(hipMemcpy(&t, c->d_tally, sizeof(t), hipMemcpyDeviceToHost));
+		*kmers = t;
+	}
+	return VC_OK;
+}
+
+extern "C" int vc_reset(vc_ctx *c)
+{
+	if (!c) return VC_EINVAL;
+	HIPCK(hipSetDevice(c->dev));
+	HIPCK(hipMemsetAsync(c->d_counts, 0, (2 * (size_t)c->n_patterns + 2) * sizeof(uint32_t), c->st));
+	HIPCK(hipMemsetAsync(c->d_tally, 0, sizeof(unsigned long long), c->st));
+	return VC_OK;
+}
+
+extern "C" void *vc_device_counts(vc_ctx *c) { return c ? (void *)c->d_counts : nullptr; }
+extern "C" void *vc_device_tally(vc_ctx *c) { return c ? (void *)c->d_tally : nullptr; }
+extern "C" void *vc_stream(vc_ctx *c) { return c ? (void *)c->st : nullptr; }
+
+extern "C" int vc_set_timing(vc_ctx *c, int enable)
+{
+	if (!c) return VC_EINVAL;
+	c->timing = enable != 0;
+	c->timed = false;
+	return VC_OK;
+}
+
+extern "C" int vc_kernel_ms(vc_ctx *c, float *ms)
+{
+	if (!c || !ms) return VC_EINVAL;
+	if (!c->timed) return VC_EINVAL;
+	HIPCK(hipEventSynchronize(c->t1));
+	HIPCK(hipEventElapsedTime(ms, c->t0, c->t1));
+	return VC_OK;
+}
+
+extern "C" int vc_table_info(const vc_ctx *c, uint64_t *n_keys, uint64_t *slots, uint64_t *filter_bytes)
+{
+	if (!c) return VC_EINVAL;
+	if (n_keys) *n_keys = c->n_keys;
+	if (slots) *slots = (uint64_t)1 << c->tbits;
+	if (filter_bytes) *filter_bytes = (uint64_t)4 << c->wbits;
+	return VC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// whole-file pass (count_fastq_kmers, vaf-counter.c:550-582)
+// ---------------------------------------------------------------------------
+
+#ifndef VC_BATCH_BYTES
+#define VC_BATCH_BYTES ((size_t)64 << 20)
+#endif
+
+namespace {
+
+// Accepted reads are written straight into a pinned slot; a full slot is
+// shipped to the device and the other slot is filled meanwhile.
+struct BatchWriter {
+	vc_ctx *c;
+	Slot *s = nullptr;
+	size_t bytes = 0;
+	uint64_t n = 0;
+	int err = VC_OK;
+
+	explicit BatchWriter(vc_ctx *ctx) : c(ctx) {}
+
+	int open_slot()
+	{
+		int rc = slot_acquire(c, &s);
+		if (rc == VC_OK) rc = slot_reserve(*s, VC_BATCH_BYTES, VC_BATCH_BYTES / 64);
+		bytes = 0;
+		n = 0;
+		return rc;
+	}
+	int flush()
+	{
+		if (!s) return VC_OK;
+		int rc = slot_submit(c, *s, bytes, n);
+		s = nullptr;
+		bytes = 0;
+		n = 0;
+		return rc;
+	}
+	int add(const char *seq, size_t len)
+	{
+		if (!s && (err = open_slot()) != VC_OK) return err;
+		if (bytes + len > s->cap_bytes || n + 1 > s->cap_reads) {
+			if (n > 0) {
+				if ((err = flush()) != VC_OK) return err;
+				if ((err = open_slot()) != VC_OK) return err;
+			}
+			if (len > s->cap_bytes && (err = slot_reserve(*s, len, 1)) != VC_OK) return err;
+		}
+		memcpy(s->h_seq + bytes, seq, len);
+		s->h_offs[n] = bytes;
+		s->h_lens[n] = (uint32_t)len;
+		bytes += len;
+		++n;
+		return VC_OK;
+	}
+};
+
+double wall_now()
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+} // namespace
+
+extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n_threads,
+                             vc_file_stats *st)
+{
+	(void)n_threads;
+	if (!c || !path) return VC_EINVAL;
+	vc_file_stats local = {0, 0, 0, 0.0};
+	const double t0 = wall_now();
+	HIPCK(hipSetDevice(c->dev));
+	VcFastqReader rd;
+	if (!rd.open(path)) return VC_EIO;
+	BatchWriter bw(c);
+	// kt_pipeline(3 workers) + worker_pipeline step 0: every worker retires
+	// on the first empty block it reads and step 0 runs strictly in block
+	// order, so a file ends at its third empty block (kthread.c:97-128,
+	// vaf-counter.c:486-517).
+	int empty = 0, rc = VC_OK;
+	while (empty < 3 && rc == VC_OK) {
+		int64_t sum = 0;
+		int ret;
+		while ((ret = rd.next()) >= 0) {
+			if (ret < c->k) continue;
+			if ((rc = bw.add(rd.seq(), (size_t)ret)) != VC_OK) break;
+			sum += ret;
+			local.bases += (uint64_t)ret;
+			local.seqs += 1;
+			if (sum >= block_bases) break;
+		}
+		if (sum == 0) ++empty;
+		else ++local.blocks;
+	}
+	if (rc == VC_OK) rc = bw.flush();
+	if (rc == VC_OK) HIPCK(hipStreamSynchronize(c->st));
+	local.seconds = wall_now() - t0;
+	if (st) *st = local;
+	return rc;
+}
+
+// ---------------------------------------------------------------------------
+// synthetic reads, misc
+// ---------------------------------------------------------------------------
+
+extern "C" int vc_synth_reads(uint8_t *d_seq, uint64_t *d_offs, uint32_t *d_lens, uint64_t first,
+                              uint64_t n_reads, uint32_t read_len, uint64_t seed, double f_snp,
+                              const uint8_t *d_windows, const uint8_t *d_dosage, uint32_t n_snp,
+                              void *stream)
+{
+	if (read_len < 1 || read_len > 301 || (n_snp && (!d_windows || !d_dosage))) return VC_EINVAL;
+	double t = f_snp * 4294967296.0;
+	uint64_t thr = t <= 0 ? 0 : (t >= 4294967296.0 ? (uint64_t)1 << 32 : (uint64_t)llround(t));
+	HIPCK(vc_launch_synth(d_seq, d_offs, d_lens, first, n_reads, read_len, seed, thr, d_windows,
+	                      d_dosage, n_snp, (hipStream_t)stream));
+	return VC_OK;
+}
+
+// Test hook: device decode of whole reads to codes (0..3, 4 = invalid).
+extern "C" int vc_debug_decode(const uint8_t *d_seq, size_t seq_bytes, const uint64_t *d_offs,
+                               const uint32_t *d_lens, uint64_t n_reads, uint8_t *d_codes, void *stream)
+{
+	HIPCK(vc_launch_decode(d_seq, seq_bytes, d_offs, d_lens, n_reads, d_codes, (hipStream_t)stream));
+	return VC_OK;
+}
+
+extern "C" const char *vc_strerror(int err)
+{
+	switch (err) {
+	case VC_OK: return "ok";
+	case VC_EINVAL: return "invalid argument";
+	case VC_ENOMEM: return "out of host memory";
+	case VC_EHIP: return "HIP runtime error";
+	case VC_ENODEV: return "no HIP device";
+	case VC_EIO: return "file could not be opened";
+	case VC_ETOOMANY: return "too many patterns";
+	default: return "unknown error";
+	}
+}
+
+extern "C" int vc_version(void) { return VAFC_VERSION_MAJOR * 100 + VAFC_VERSION_MINOR; }

@@ -1,0 +1,54 @@
+// vafc_internal.h -- kernel argument block and launchers shared by the host
+// library (vafc_host.cpp) and the kernels (vafc_kernels.hip).  Not part of
+// the public C ABI (include/vafc.h).
+#ifndef VAFC_INTERNAL_H
+#define VAFC_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#define VC_BLOCK 1024        // threads per block: 16 waves, one block per CU
+#define VC_QCAP 128          // per-wave LDS queue entries
+
+struct VcKernelArgs {
+	const uint8_t *seq;          // 4-byte aligned base of the read bytes
+	uint64_t seq_words;          // readable dwords from seq
+	uint64_t off_adj;            // added to every offset (seq realignment)
+	const uint64_t *offs;
+	const uint32_t *lens;
+	uint64_t n_reads;
+	const uint64_t *tkeys;       // exact table, 2^tbits slots, VC_EMPTY_KEY = empty
+	const uint32_t *tvals;
+	uint32_t tbits, tmask;
+	const uint32_t *filter;      // 2^wbits words
+	uint32_t wbits;
+	int k;
+	uint64_t kmask;              // (1 << 2k) - 1
+	uint32_t *counts;            // [2 * n_patterns]
+	unsigned long long *tally;   // valid k-mers extracted
+	uint32_t *nlong;             // long-read list fill (zeroed per launch)
+	uint32_t *longlist;
+	uint32_t long_cap;
+};
+
+static inline size_t vc_lds_bytes(uint32_t wbits)
+{
+	return ((size_t)4 << wbits) + (size_t)(VC_BLOCK / 64) * VC_QCAP * 8;
+}
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+hipError_t vc_kernel_setup(void);
+hipError_t vc_launch_count(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st);
+hipError_t vc_launch_decode(const uint8_t *seq, uint64_t seq_bytes, const uint64_t *offs,
+                            const uint32_t *lens, uint64_t n_reads, uint8_t *codes, hipStream_t st);
+hipError_t vc_launch_synth(uint8_t *seq, uint64_t *offs, uint32_t *lens, uint64_t first,
+                           uint64_t n_reads, uint32_t L, uint64_t seed, uint64_t thr,
+                           const uint8_t *win, const uint8_t *dosage, uint32_t n_snp, hipStream_t st);
+#ifdef __cplusplus
+}
+#endif
+
+#endif

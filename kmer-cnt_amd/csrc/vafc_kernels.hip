@@ -1,0 +1,489 @@
+// vafc_kernels.hip -- HIP kernels of the vaf-counter hot path for gfx950 (CDNA4).
+//
+// Replaces steps 1+2 of the reference pipeline: the SSSE3 2-bit encode
+// (vaf-counter.c:261-291), the rolling canonical k-mer extraction
+// (vaf-counter.c:349-427) and the khashl lookup + relaxed atomic increment
+// (vaf-counter.c:449-479, khashl.h:137-150).  Integer work only, no MFMA.
+//
+// Design (DESIGN.md has the full story):
+//  * One lane per read, one wave = 64 reads, 1024-thread persistent blocks
+//    (one per CU, 16 waves/CU) grid-striding over groups of 1024 reads.
+//  * Read bytes are fetched as dwords from the read's 4-byte-aligned start and
+//    realigned with v_alignbyte; 16 bases (one "chunk") per loop trip, with
+//    the next chunk's dwords in flight during the current one.
+//  * Decode is SWAR on 4 bytes at a time with v_perm_b32 as a 8-entry LUT --
+//    the same nibble table as the reference's PSHUFB; the reference decodes
+//    the last len%16 bytes of a read with seq_nt4_table instead, so the lane
+//    switches to an exact SWAR seq_nt4_table for that tail chunk.
+//  * Rolling forward / reverse-complement k-mers in 64-bit registers; validity
+//    from a 32-bit shift register of invalid-base flags (a window is valid iff
+//    its last k flags are zero) -- equivalent to the reference's reset-on-N.
+//  * Every valid canonical k-mer probes a blocked Bloom filter held in LDS
+//    (2 bits in one 32-bit word, up to 128 KiB).  Filter hits are compacted
+//    per wave into an LDS queue (ballot + mbcnt); a full queue is drained by
+//    all 64 lanes probing the exact HBM/L2-resident table at once, and hits do
+//    atomicAdd on uint32 counts[(pattern<<1)|is_alt].
+//  * Reads longer than VC_LONG_READ are appended to a list and counted by a
+//    second kernel in which every lane of the grid takes a VC_LONG_SEG-base
+//    segment (plus a k-1 halo) of the read.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "vafc_common.h"
+#include "vafc_internal.h"
+
+#define WAVE 64
+#define QCAP 128            // per-wave LDS queue entries (u64)
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ int wave_max_i32(int v)
+{
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) {
+		int u = __shfl_xor(v, o, WAVE);
+		v = u > v ? u : v;
+	}
+	return v;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
+{
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+	return v;
+}
+
+// Nibble LUT of the reference's PSHUFB decode (vaf-counter.c:272-275) for
+// low nibbles 0..7, {4,0,4,1,3,3,4,2}; nibbles 8..15 are all 4 (invalid).
+// v_perm_b32 selector bytes 0..3 pick bytes of the 2nd operand, 4..7 of the 1st.
+#define NIB_LO 0x01040004u
+#define NIB_HI 0x02040303u
+// Expected high nibble (with the lower-case bit cleared) of an ACGTU letter
+// for each low nibble 0..7; 0xFF never matches.
+#define LET_LO 0x04FF04FFu
+#define LET_HI 0x04FF0505u
+
+// Head decode of 4 bytes: code byte = LUT[b & 15]; bit 2 set <=> invalid.
+__device__ __forceinline__ uint32_t dec_head(uint32_t b)
+{
+	uint32_t t = __builtin_amdgcn_perm(NIB_HI, NIB_LO, b & 0x07070707u);
+	return t | ((b >> 1) & 0x04040404u);
+}
+
+// Tail decode = seq_nt4_table (vaf-counter.c:73-90) on 4 bytes: ACGTU/acgtu
+// keep their nibble code, bytes 0..3 map to themselves, all else invalid.
+__device__ __forceinline__ uint32_t dec_tail(uint32_t b)
+{
+	uint32_t t = dec_head(b);
+	uint32_t e = __builtin_amdgcn_perm(LET_HI, LET_LO, b & 0x07070707u);
+	uint32_t m = ((b >> 4) & 0x0D0D0D0Du) ^ e;
+	uint32_t nz = (((m & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | m) & 0x80808080u;  // byte != 0
+	t |= nz >> 5;
+	uint32_t y = b & 0xFCFCFCFCu;
+	uint32_t small = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u; // byte < 4
+	uint32_t sel = (small >> 7) * 0xFFu;
+	return (t & ~sel) | (b & sel);
+}
+
+// Invalid-flag mask for the bytes of a word whose first position is P, given
+// the valid position range [lo, hi): bytes outside get bit 2 set.
+__device__ __forceinline__ uint32_t range_mask_hi(int rel_hi)
+{
+	// bytes i >= rel_hi are outside
+	return rel_hi >= 4 ? 0u : (rel_hi <= 0 ? 0x04040404u : (0x04040404u << (8 * rel_hi)));
+}
+__device__ __forceinline__ uint32_t range_mask_lo(int rel_lo)
+{
+	// bytes i < rel_lo are outside
+	return rel_lo <= 0 ? 0u : (rel_lo >= 4 ? 0x04040404u : (0x04040404u & ((1u << (8 * rel_lo)) - 1u)));
+}
+
+__device__ __forceinline__ uint32_t ldw(const uint32_t *__restrict__ s32, uint64_t i, uint64_t wmax)
+{
+	return s32[i < wmax ? i : wmax];
+}
+
+// ---------------------------------------------------------------------------
+// exact table probe (drain side)
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ void probe_and_count(const VcKernelArgs &A, uint64_t key)
+{
+	uint32_t h = vc_hash(key);
+	uint32_t s = vc_table_slot(h, A.tbits);
+	for (;;) {
+		uint64_t k2 = A.tkeys[s];
+		if (k2 == key) {
+			atomicAdd(&A.counts[A.tvals[s]], 1u);
+			break;
+		}
+		if (k2 == VC_EMPTY_KEY) break;
+		s = (s + 1u) & A.tmask;
+	}
+}
+
+struct WaveQueue {
+	uint64_t *q;     // LDS, QCAP entries
+	uint32_t n;      // wave-uniform fill
+};
+
+__device__ __forceinline__ void queue_push(const VcKernelArgs &A, WaveQueue &Q, bool hit,
+                                           uint64_t key, int lane)
+{
+	uint64_t bal = __ballot(hit);
+	if (bal) {
+		uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+		                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+		if (hit) Q.q[Q.n + pre] = key;
+		Q.n += (uint32_t)__popcll(bal);
+		if (Q.n >= WAVE) {
+			__builtin_amdgcn_wave_barrier();
+			uint64_t k0 = Q.q[lane];
+			uint32_t rest = Q.n - WAVE;
+			uint64_t k1 = Q.q[lane + WAVE];
+			__builtin_amdgcn_wave_barrier();
+			if ((uint32_t)lane < rest) Q.q[lane] = k1;
+			Q.n = rest;
+			probe_and_count(A, k0);
+		}
+	}
+}
+
+__device__ __forceinline__ void queue_flush(const VcKernelArgs &A, WaveQueue &Q, int lane)
+{
+	__builtin_amdgcn_wave_barrier();
+	if ((uint32_t)lane < Q.n) probe_and_count(A, Q.q[lane]);
+	Q.n = 0;
+}
+
+// ---------------------------------------------------------------------------
+// scan one span of one read per lane, wave-uniform trip count
+// ---------------------------------------------------------------------------
+//
+// Lane processes chunks [c_lo, c_hi) of its read (chunk c = read positions
+// 16c..16c+15), emitting the canonical k-mers whose whole window lies in the
+// valid position range [vlo, vhi) (vlo = 0, vhi = len for a whole read).
+template <bool HAS_LO>
+__device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
+                                          uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
+                                          int vlo, int vhi, int nit, const uint32_t *__restrict__ filt,
+                                          WaveQueue &Q, uint32_t &tally, int lane)
+{
+	const int k = A.k;
+	const uint64_t kmask = A.kmask;
+	const uint32_t rsh = 2u * (uint32_t)(k - 1);
+	const uint32_t kshl = 32u - (uint32_t)k;
+	const uint32_t wsh = 32u - A.wbits, b1s = 27u - A.wbits, b2s = 22u - A.wbits;
+	const int tail_c = (len & 15) ? (len >> 4) : -1;
+
+	uint64_t addr = off + 16ull * (uint64_t)c_lo;
+	uint64_t wi = addr >> 2;
+	uint32_t sh = (uint32_t)(addr & 3u);
+	bool act = c_lo < c_hi;
+	uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
+	if (act) {
+		w0 = ldw(s32, wi, wmax); w1 = ldw(s32, wi + 1, wmax); w2 = ldw(s32, wi + 2, wmax);
+		w3 = ldw(s32, wi + 3, wmax); w4 = ldw(s32, wi + 4, wmax);
+	}
+	uint64_t fwd = 0, rev = 0;
+	uint32_t inv = 0xFFFFFFFFu;
+
+	for (int it = 0; it < nit; ++it) {
+		const int c = c_lo + it;
+		act = c < c_hi;
+		// next chunk's words (w4 becomes the next w0)
+		uint32_t x1 = 0, x2 = 0, x3 = 0, x4 = 0;
+		if (c + 1 < c_hi) {
+			x1 = ldw(s32, wi + 5, wmax); x2 = ldw(s32, wi + 6, wmax);
+			x3 = ldw(s32, wi + 7, wmax); x4 = ldw(s32, wi + 8, wmax);
+		}
+		uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+		uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+		uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+		uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
+		uint32_t t0, t1, t2, t3;
+		if (c == tail_c) {
+			t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3);
+		} else {
+			t0 = dec_head(b0); t1 = dec_head(b1); t2 = dec_head(b2); t3 = dec_head(b3);
+		}
+		const int P = 16 * c;
+		t0 |= range_mask_hi(vhi - P);
+		t1 |= range_mask_hi(vhi - P - 4);
+		t2 |= range_mask_hi(vhi - P - 8);
+		t3 |= range_mask_hi(vhi - P - 12);
+		if (HAS_LO) {
+			t0 |= range_mask_lo(vlo - P);
+			t1 |= range_mask_lo(vlo - P - 4);
+			t2 |= range_mask_lo(vlo - P - 8);
+			t3 |= range_mask_lo(vlo - P - 12);
+		}
+		if (!act) { t0 = t1 = t2 = t3 = 0x04040404u; }
+
+#pragma unroll
+		for (int j = 0; j < 16; ++j) {
+			const uint32_t tw = j < 4 ? t0 : (j < 8 ? t1 : (j < 12 ? t2 : t3));
+			const uint32_t x = tw >> (8 * (j & 3));
+			const uint32_t cb = x & 3u;
+			const uint32_t bad = (x >> 2) & 1u;
+			fwd = ((fwd << 2) | cb) & kmask;
+			rev = (rev >> 2) | ((uint64_t)(cb ^ 3u) << rsh);
+			inv = (inv << 1) | bad;
+			const bool valid = (inv << kshl) == 0u;
+			const uint64_t can = fwd < rev ? fwd : rev;
+			const uint32_t h = vc_hash(can);
+			const uint32_t fw = filt[h >> wsh];
+			const uint32_t fm = (1u << ((h >> b1s) & 31u)) | (1u << ((h >> b2s) & 31u));
+			const bool hit = valid && ((fw & fm) == fm);
+			tally += valid ? 1u : 0u;
+			queue_push(A, Q, hit, can, lane);
+		}
+		w0 = w4; w1 = x1; w2 = x2; w3 = x3; w4 = x4;
+		wi += 4;
+	}
+}
+
+__device__ __forceinline__ void load_filter(const VcKernelArgs &A, uint32_t *filt)
+{
+	const uint32_t nw = 1u << A.wbits;
+	const uint4 *src = reinterpret_cast<const uint4 *>(A.filter);
+	uint4 *dst = reinterpret_cast<uint4 *>(filt);
+	for (uint32_t i = threadIdx.x; i < nw / 4u; i += blockDim.x) dst[i] = src[i];
+	__syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// kernel 1: whole reads, one lane per read
+// ---------------------------------------------------------------------------
+
+__global__ void __launch_bounds__(VC_BLOCK)
+vc_count_reads_kernel(VcKernelArgs A)
+{
+	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+	uint32_t *filt = smem;
+	const int lane = threadIdx.x & (WAVE - 1);
+	const int wave = threadIdx.x / WAVE;
+	WaveQueue Q;
+	Q.q = reinterpret_cast<uint64_t *>(smem + (1u << A.wbits)) + wave * QCAP;
+	Q.n = 0;
+	load_filter(A, filt);
+
+	const uint32_t *s32 = reinterpret_cast<const uint32_t *>(A.seq);
+	const uint64_t wmax = A.seq_words ? A.seq_words - 1 : 0;
+	unsigned long long tally_all = 0;
+
+	for (uint64_t g = blockIdx.x; g * (uint64_t)VC_BLOCK < A.n_reads; g += gridDim.x) {
+		const uint64_t r = g * (uint64_t)VC_BLOCK + threadIdx.x;
+		int len = 0;
+		uint64_t off = 0;
+		if (r < A.n_reads) {
+			len = (int)A.lens[r];
+			off = A.offs[r] + A.off_adj;
+			if ((uint32_t)len > VC_LONG_READ) {
+				uint32_t slot = atomicAdd(A.nlong, 1u);
+				if (slot < A.long_cap) A.longlist[slot] = (uint32_t)r;
+				len = 0;
+			}
+		}
+		const int nch = (len + 15) >> 4;
+		const int nit = wave_max_i32(nch);
+		uint32_t tally = 0;
+		scan_span<false>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tally, lane);
+		tally_all += tally;
+	}
+	queue_flush(A, Q, lane);
+	tally_all = wave_sum_u64(tally_all);
+	if (lane == 0 && tally_all) atomicAdd(A.tally, tally_all);
+}
+
+// ---------------------------------------------------------------------------
+// kernel 2: long reads, every lane of the grid takes one segment
+// ---------------------------------------------------------------------------
+
+__global__ void __launch_bounds__(VC_BLOCK)
+vc_count_long_kernel(VcKernelArgs A)
+{
+	const uint32_t nl_raw = *A.nlong;
+	const uint32_t nl = nl_raw < A.long_cap ? nl_raw : A.long_cap;
+	if (nl == 0) return;   // uniform over the grid
+	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+	uint32_t *filt = smem;
+	const int lane = threadIdx.x & (WAVE - 1);
+	const int wave = threadIdx.x / WAVE;
+	WaveQueue Q;
+	Q.q = reinterpret_cast<uint64_t *>(smem + (1u << A.wbits)) + wave * QCAP;
+	Q.n = 0;
+	load_filter(A, filt);
+
+	const uint32_t *s32 = reinterpret_cast<const uint32_t *>(A.seq);
+	const uint64_t wmax = A.seq_words ? A.seq_words - 1 : 0;
+	const int k = A.k;
+	unsigned long long tally_all = 0;
+	const uint64_t stride = (uint64_t)gridDim.x * VC_BLOCK;
+
+	for (uint32_t li = 0; li < nl; ++li) {
+		const uint32_t r = A.longlist[li];
+		const int len = (int)A.lens[r];
+		const uint64_t off = A.offs[r] + A.off_adj;
+		const uint64_t nseg = ((uint64_t)len + VC_LONG_SEG - 1) / VC_LONG_SEG;
+		for (uint64_t s0 = (uint64_t)blockIdx.x * VC_BLOCK; s0 < nseg; s0 += stride) {
+			const uint64_t s = s0 + threadIdx.x;
+			int vlo = 0, vhi = 0, c_lo = 0, c_hi = 0;
+			if (s < nseg) {
+				const int64_t e0 = (int64_t)s * VC_LONG_SEG;
+				const int64_t e1 = e0 + VC_LONG_SEG < len ? e0 + VC_LONG_SEG : len;
+				vlo = (int)(e0 - (k - 1) > 0 ? e0 - (k - 1) : 0);
+				vhi = (int)e1;
+				c_lo = vlo >> 4;
+				c_hi = (vhi + 15) >> 4;
+			}
+			const int nit = wave_max_i32(c_hi - c_lo);
+			uint32_t tally = 0;
+			scan_span<true>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tally, lane);
+			tally_all += tally;
+		}
+	}
+	queue_flush(A, Q, lane);
+	tally_all = wave_sum_u64(tally_all);
+	if (lane == 0 && tally_all) atomicAdd(A.tally, tally_all);
+}
+
+// ---------------------------------------------------------------------------
+// debug kernel: position-dependent decode of whole reads (tests only)
+// ---------------------------------------------------------------------------
+
+__global__ void vc_decode_kernel(const uint8_t *seq, uint64_t seq_bytes, const uint64_t *offs,
+                                 const uint32_t *lens, uint64_t n_reads, uint8_t *codes)
+{
+	const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (r >= n_reads) return;
+	const uint32_t *s32 = reinterpret_cast<const uint32_t *>(seq);
+	const uint64_t nw = (seq_bytes + 3) / 4;
+	const uint64_t wmax = nw ? nw - 1 : 0;
+	const int len = (int)lens[r];
+	const uint64_t off = offs[r];
+	const int tail_c = (len & 15) ? (len >> 4) : -1;
+	for (int c = 0; 16 * c < len; ++c) {
+		uint64_t addr = off + 16ull * c;
+		uint64_t wi = addr >> 2;
+		uint32_t sh = (uint32_t)(addr & 3u);
+		uint32_t w[5];
+		for (int j = 0; j < 5; ++j) w[j] = ldw(s32, wi + j, wmax);
+		for (int m = 0; m < 4; ++m) {
+			uint32_t b = __builtin_amdgcn_alignbyte(w[m + 1], w[m], sh);
+			uint32_t t = (c == tail_c) ? dec_tail(b) : dec_head(b);
+			for (int i = 0; i < 4; ++i) {
+				int p = 16 * c + 4 * m + i;
+				if (p < len) {
+					uint32_t cb = (t >> (8 * i)) & 0xFFu;
+					codes[off + p] = (cb & 4u) ? 4u : (uint8_t)(cb & 3u);
+				}
+			}
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------
+// synthetic reads (vafc_synth.py on the device)
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint64_t h64(uint64_t seed, uint64_t item, uint64_t draw)
+{
+	uint64_t z = seed * 0x9E3779B97F4A7C15ull + item * 0xD1B54A32D192ED03ull + draw * 0xABC98388FB8FAC03ull;
+	z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+	z ^= z >> 27; z *= 0x94D049BB133111EBull;
+	z ^= z >> 31;
+	return z;
+}
+
+__global__ void vc_synth_kernel(uint8_t *seq, uint64_t *offs, uint32_t *lens, uint64_t first,
+                                uint64_t n_reads, uint32_t L, uint64_t seed, uint64_t thr,
+                                const uint8_t *win, const uint8_t *dosage, uint32_t n_snp)
+{
+	const uint64_t total = n_reads * (uint64_t)L;
+	const uint64_t THR_N = 4294967ull, THR_SUB = 25769803ull;
+	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+	     i += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t rd = i / L;
+		const uint32_t p = (uint32_t)(i - rd * L);
+		const uint64_t ri = first + rd;
+		const uint64_t r0 = h64(seed, ri, 0), r1 = h64(seed, ri, 1);
+		const uint64_t r2 = h64(seed, ri, 2), r3 = h64(seed, ri, 3);
+		const bool rc = (r3 & 1ull) != 0;
+		const uint32_t q = rc ? L - 1u - p : p;
+		const uint64_t r = h64(seed, ri, 16ull + q);
+		uint32_t base = (uint32_t)(r & 3ull);
+		const bool is_snp = n_snp > 0 && (r0 >> 32) < thr;
+		if (is_snp) {
+			const uint64_t snp = ((r1 >> 32) * (uint64_t)n_snp) >> 32;
+			const uint32_t g = dosage[snp];
+			const bool alt = g == 2u || (g == 1u && (r1 & 1ull));
+			const uint64_t nstart = 301u - L + 1u;
+			const uint64_t start = ((r2 >> 32) * nstart) >> 32;
+			const uint8_t ch = win[(snp * 2u + (alt ? 1u : 0u)) * 301u + start + q];
+			base = ch == 'A' ? 0u : ch == 'C' ? 1u : ch == 'G' ? 2u : 3u;
+		}
+		const uint64_t u = r >> 32;
+		if (u >= THR_N && u < THR_SUB) base = (base + 1u + (uint32_t)(((r >> 2) & 0xFFFFull) % 3ull)) & 3u;
+		uint8_t out;
+		if (u < THR_N) out = 'N';
+		else {
+			if (rc) base ^= 3u;
+			out = "ACGT"[base];
+		}
+		seq[i] = out;
+		if (p == 0) { offs[rd] = rd * (uint64_t)L; lens[rd] = L; }
+	}
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+
+extern "C" hipError_t vc_launch_count(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
+{
+	const size_t lds = vc_lds_bytes(A->wbits);
+	hipLaunchKernelGGL(vc_count_reads_kernel, dim3(grid), dim3(VC_BLOCK), lds, st, *A);
+	hipError_t e = hipGetLastError();
+	if (e != hipSuccess) return e;
+	hipLaunchKernelGGL(vc_count_long_kernel, dim3(grid_long), dim3(VC_BLOCK), lds, st, *A);
+	return hipGetLastError();
+}
+
+extern "C" hipError_t vc_kernel_setup(void)
+{
+	const size_t lds = vc_lds_bytes(VC_MAX_FILTER_WBITS);
+	hipError_t e = hipFuncSetAttribute((const void *)vc_count_reads_kernel,
+	                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+	if (e != hipSuccess) return e;
+	return hipFuncSetAttribute((const void *)vc_count_long_kernel,
+	                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+}
+
+extern "C" hipError_t vc_launch_decode(const uint8_t *seq, uint64_t seq_bytes, const uint64_t *offs,
+                                       const uint32_t *lens, uint64_t n_reads, uint8_t *codes,
+                                       hipStream_t st)
+{
+	const int blk = 256;
+	const int grid = (int)((n_reads + blk - 1) / blk);
+	if (grid == 0) return hipSuccess;
+	hipLaunchKernelGGL(vc_decode_kernel, dim3(grid), dim3(blk), 0, st, seq, seq_bytes, offs, lens,
+	                   n_reads, codes);
+	return hipGetLastError();
+}
+
+extern "C" hipError_t vc_launch_synth(uint8_t *seq, uint64_t *offs, uint32_t *lens, uint64_t first,
+                                      uint64_t n_reads, uint32_t L, uint64_t seed, uint64_t thr,
+                                      const uint8_t *win, const uint8_t *dosage, uint32_t n_snp,
+                                      hipStream_t st)
+{
+	const uint64_t total = n_reads * (uint64_t)L;
+	if (total == 0) return hipSuccess;
+	uint64_t blocks = (total + 255) / 256;
+	if (blocks > 65536) blocks = 65536;
+	hipLaunchKernelGGL(vc_synth_kernel, dim3((unsigned)blocks), dim3(256), 0, st, seq, offs, lens,
+	                   first, n_reads, L, seed, thr, win, dosage, n_snp);
+	return hipGetLastError();
+}
