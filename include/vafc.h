@@ -121,6 +121,10 @@ int vc_reset(vc_ctx *ctx);
 /* Device pointer of the uint32 counts[2*n_patterns] array (for a device-side
  * all-reduce across ranks, e.g. RCCL through torch.distributed). */
 void *vc_device_counts(vc_ctx *ctx);
+/* Count into caller-owned device buffers instead (uint32[2*n_patterns] and
+ * one uint64), e.g. torch tensors that an RCCL all-reduce then sums across
+ * ranks; NULL restores the ctx's own buffers.  Not zeroed by this call. */
+int vc_bind_outputs(vc_ctx *ctx, void *d_counts, void *d_tally);
 void *vc_device_tally(vc_ctx *ctx);
 void *vc_stream(vc_ctx *ctx);
 

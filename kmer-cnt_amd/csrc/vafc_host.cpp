@@ -234,8 +234,10 @@ struct vc_ctx {
 	uint32_t tbits = 0;
 	uint32_t *d_filter = nullptr;
 	uint32_t wbits = 0;
-	uint32_t *d_counts = nullptr;
+	uint32_t *d_counts = nullptr;          // active outputs (own or bound)
 	unsigned long long *d_tally = nullptr;
+	uint32_t *own_counts = nullptr;
+	unsigned long long *own_tally = nullptr;
 	uint32_t *d_nlong = nullptr;
 	uint32_t *d_long = nullptr;
 	uint32_t long_cap = 0;
@@ -323,8 +325,10 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	TRY(hipMalloc(&c->d_tkeys, tslots * sizeof(uint64_t)));
 	TRY(hipMalloc(&c->d_tvals, tslots * sizeof(uint32_t)));
 	TRY(hipMalloc(&c->d_filter, fw.size() * sizeof(uint32_t)));
-	TRY(hipMalloc(&c->d_counts, (2 * (size_t)n_patterns + 2) * sizeof(uint32_t)));
-	TRY(hipMalloc(&c->d_tally, sizeof(unsigned long long)));
+	TRY(hipMalloc(&c->own_counts, (2 * (size_t)n_patterns + 2) * sizeof(uint32_t)));
+	TRY(hipMalloc(&c->own_tally, sizeof(unsigned long long)));
+	c->d_counts = c->own_counts;
+	c->d_tally = c->own_tally;
 	TRY(hipMalloc(&c->d_nlong, sizeof(uint32_t)));
 	TRY(hipMemcpy(c->d_tkeys, tk.data(), tslots * sizeof(uint64_t), hipMemcpyHostToDevice));
 	TRY(hipMemcpy(c->d_tvals, tv.data(), tslots * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -375,8 +379,8 @@ extern "C" void vc_destroy(vc_ctx *c)
 	if (c->d_tkeys) (void)hipFree(c->d_tkeys);
 	if (c->d_tvals) (void)hipFree(c->d_tvals);
 	if (c->d_filter) (void)hipFree(c->d_filter);
-	if (c->d_counts) (void)hipFree(c->d_counts);
-	if (c->d_tally) (void)hipFree(c->d_tally);
+	if (c->own_counts) (void)hipFree(c->own_counts);
+	if (c->own_tally) (void)hipFree(c->own_tally);
 	if (c->d_nlong) (void)hipFree(c->d_nlong);
 	if (c->d_long) (void)hipFree(c->d_long);
 	if (c->st) (void)hipStreamDestroy(c->st);
@@ -520,12 +524,20 @@ extern "C" int vc_reset(vc_ctx *c)
 {
 	if (!c) return VC_EINVAL;
 	HIPCK(hipSetDevice(c->dev));
-	HIPCK(hipMemsetAsync(c->d_counts, 0, (2 * (size_t)c->n_patterns + 2) * sizeof(uint32_t), c->st));
+	HIPCK(hipMemsetAsync(c->d_counts, 0, 2 * (size_t)c->n_patterns * sizeof(uint32_t), c->st));
 	HIPCK(hipMemsetAsync(c->d_tally, 0, sizeof(unsigned long long), c->st));
 	return VC_OK;
 }
 
 extern "C" void *vc_device_counts(vc_ctx *c) { return c ? (void *)c->d_counts : nullptr; }
+extern "C" int vc_bind_outputs(vc_ctx *c, void *d_counts, void *d_tally)
+{
+	if (!c) return VC_EINVAL;
+	c->d_counts = d_counts ? (uint32_t *)d_counts : c->own_counts;
+	c->d_tally = d_tally ? (unsigned long long *)d_tally : c->own_tally;
+	return VC_OK;
+}
+
 extern "C" void *vc_device_tally(vc_ctx *c) { return c ? (void *)c->d_tally : nullptr; }
 extern "C" void *vc_stream(vc_ctx *c) { return c ? (void *)c->st : nullptr; }
 

@@ -1,0 +1,415 @@
+"""Python host mirror of the MI355X vaf-counter hot path (ctypes over libvafc.so).
+
+This mirrors the reference's own interface for the path, function by function
+(gerbenvoshol/kmer-cnt, vaf-counter.c):
+
+=============================  ==========================================  ===================
+reference (vaf-counter.c)       here                                        C ABI (include/vafc.h)
+=============================  ==========================================  ===================
+load_patterns        :149      ``load_patterns(fn)``                       vc_patterns_load
+create_combined_kmer_map :198  ``create_combined_kmer_map(db, k)``         vc_patterns_keys + vc_create
+count_fastq_kmers    :550      ``count_fastq_kmers(fn, k, t, b, map, db)`` vc_count_file
+worker_pipeline steps 1+2      ``KmerMap.count_block / count_device``      vc_count_block / vc_count_device
+main  :584-738                 ``main(argv)``                              (all of the above) + vc_write_vaf
+=============================  ==========================================  ===================
+
+Everything that counts goes through the HIP kernels of ``libvafc.so``; if the
+library is missing this module raises ``VafcError`` -- there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import sys
+import time
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("VAFC_LIB", os.path.join(_HERE, "lib", "libvafc.so"))
+
+VC_OK, VC_EINVAL, VC_ENOMEM, VC_EHIP, VC_ENODEV, VC_EIO, VC_ETOOMANY = 0, -1, -2, -3, -4, -5, -6
+
+# every symbol include/vafc.h declares
+EXPORTS = (
+    "vc_patterns_load", "vc_patterns_free", "vc_patterns_count", "vc_patterns_keys",
+    "vc_write_vaf", "vc_pattern_fields", "vc_free", "vc_create", "vc_destroy",
+    "vc_count_block", "vc_count_device", "vc_finish", "vc_reset", "vc_device_counts",
+    "vc_bind_outputs", "vc_device_tally", "vc_stream", "vc_set_timing", "vc_kernel_ms",
+    "vc_table_info", "vc_count_file", "vc_synth_reads", "vc_debug_decode", "vc_strerror",
+    "vc_version",
+)
+
+
+class VafcError(RuntimeError):
+    def __init__(self, what, code=None):
+        if code is not None:
+            what = "%s: %s (%d)" % (what, lib().vc_strerror(code).decode(), code)
+        super().__init__(what)
+        self.code = code
+
+
+class FileStats(C.Structure):
+    _fields_ = [("bases", C.c_uint64), ("seqs", C.c_uint64), ("blocks", C.c_uint64),
+                ("seconds", C.c_double)]
+
+
+_lib = None
+P = C.c_void_p
+
+
+def lib():
+    """Load libvafc.so (built by ``make -C kmer-cnt_amd/csrc``); raise if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise VafcError("libvafc.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+    # torch bundles its own libamdhip64.so.7; loading it first makes libvafc.so
+    # bind to that same runtime (one HIP runtime per process).  Loading
+    # libvafc.so first would let torch map a second copy later.
+    if os.environ.get("VAFC_NO_TORCH", "0") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+    L = C.CDLL(LIB_PATH)
+    sig = {
+        "vc_patterns_load": (C.c_int, [C.c_char_p, C.POINTER(P)]),
+        "vc_patterns_free": (None, [P]),
+        "vc_patterns_count": (C.c_int, [P]),
+        "vc_patterns_keys": (C.c_int, [P, C.c_int, C.POINTER(P), C.POINTER(P),
+                                       C.POINTER(C.c_size_t), C.POINTER(C.c_int)]),
+        "vc_write_vaf": (C.c_int, [P, P, C.c_char_p]),
+        "vc_pattern_fields": (C.c_int, [P, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_int),
+                                        C.POINTER(C.c_char_p), C.POINTER(C.c_char),
+                                        C.POINTER(C.c_char), C.POINTER(C.c_char_p),
+                                        C.POINTER(C.c_char_p)]),
+        "vc_free": (None, [P]),
+        "vc_create": (C.c_int, [C.POINTER(P), C.c_int, P, P, C.c_size_t, C.c_uint32, C.c_int]),
+        "vc_destroy": (None, [P]),
+        "vc_count_block": (C.c_int, [P, P, C.c_size_t, P, P, C.c_uint64]),
+        "vc_count_device": (C.c_int, [P, P, C.c_size_t, P, P, C.c_uint64, P]),
+        "vc_finish": (C.c_int, [P, P, C.POINTER(C.c_uint64)]),
+        "vc_reset": (C.c_int, [P]),
+        "vc_device_counts": (P, [P]),
+        "vc_bind_outputs": (C.c_int, [P, P, P]),
+        "vc_device_tally": (P, [P]),
+        "vc_stream": (P, [P]),
+        "vc_set_timing": (C.c_int, [P, C.c_int]),
+        "vc_kernel_ms": (C.c_int, [P, C.POINTER(C.c_float)]),
+        "vc_table_info": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                    C.POINTER(C.c_uint64)]),
+        "vc_count_file": (C.c_int, [P, C.c_char_p, C.c_int, C.c_int, C.POINTER(FileStats)]),
+        "vc_synth_reads": (C.c_int, [P, P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
+                                     C.c_double, P, P, C.c_uint32, P]),
+        "vc_debug_decode": (C.c_int, [P, C.c_size_t, P, P, C.c_uint64, P, P]),
+        "vc_strerror": (C.c_char_p, [C.c_int]),
+        "vc_version": (C.c_int, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _ck(rc, what):
+    if rc != VC_OK:
+        raise VafcError(what, rc)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(P)
+
+
+# --------------------------------------------------------------------------
+# pattern database
+# --------------------------------------------------------------------------
+
+class PatternDB:
+    """patterns.txt records (vaf-counter.c:92-108,149-184)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @property
+    def n(self) -> int:
+        return lib().vc_patterns_count(self._h)
+
+    def __len__(self):
+        return self.n
+
+    def record(self, i: int):
+        chr_, rsid, rk, ak = C.c_char_p(), C.c_char_p(), C.c_char_p(), C.c_char_p()
+        start, ref, alt = C.c_int(), C.c_char(), C.c_char()
+        _ck(lib().vc_pattern_fields(self._h, i, C.byref(chr_), C.byref(start), C.byref(rsid),
+                                    C.byref(ref), C.byref(alt), C.byref(rk), C.byref(ak)),
+            "vc_pattern_fields")
+        return (chr_.value.decode("latin-1"), start.value, rsid.value.decode("latin-1"),
+                ref.value, alt.value, rk.value, ak.value)
+
+    def keys(self, k: int):
+        """(keys uint64[m], vals uint32[m], n_collisions) -- create_combined_kmer_map's content."""
+        kp, vp, n, coll = P(), P(), C.c_size_t(), C.c_int()
+        _ck(lib().vc_patterns_keys(self._h, k, C.byref(kp), C.byref(vp), C.byref(n), C.byref(coll)),
+            "vc_patterns_keys")
+        try:
+            m = n.value
+            keys = np.ctypeslib.as_array(C.cast(kp, C.POINTER(C.c_uint64)), (m,)).copy() if m else \
+                np.zeros(0, np.uint64)
+            vals = np.ctypeslib.as_array(C.cast(vp, C.POINTER(C.c_uint32)), (m,)).copy() if m else \
+                np.zeros(0, np.uint32)
+        finally:
+            lib().vc_free(kp)
+            lib().vc_free(vp)
+        return keys, vals, coll.value
+
+    def write_vaf(self, counts: np.ndarray, path: str) -> None:
+        counts = np.ascontiguousarray(counts, dtype=np.uint32)
+        assert counts.size >= 2 * self.n
+        _ck(lib().vc_write_vaf(self._h, _ptr(counts), path.encode()), "vc_write_vaf")
+
+    def close(self):
+        if self._h:
+            lib().vc_patterns_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def load_patterns(fn: str) -> PatternDB:
+    """load_patterns (vaf-counter.c:149): raises VafcError(VC_EIO) if unreadable."""
+    h = P()
+    _ck(lib().vc_patterns_load(fn.encode(), C.byref(h)), "load_patterns(%s)" % fn)
+    return PatternDB(h)
+
+
+# --------------------------------------------------------------------------
+# device k-mer map + counters
+# --------------------------------------------------------------------------
+
+class KmerMap:
+    """The device-resident static key table + counts (kmer_cnt_t + pattern_t counters)."""
+
+    def __init__(self, k: int, keys: np.ndarray, vals: np.ndarray, n_patterns: int, device: int = 0):
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        vals = np.ascontiguousarray(vals, dtype=np.uint32)
+        self.k, self.n_patterns, self.device = k, int(n_patterns), device
+        h = P()
+        _ck(lib().vc_create(C.byref(h), k, _ptr(keys), _ptr(vals), keys.size, self.n_patterns, device),
+            "vc_create")
+        self._h = h
+        self.n_collisions = 0
+
+    # -- counting -----------------------------------------------------------
+    def count_block(self, seq: np.ndarray, offs: np.ndarray, lens: np.ndarray) -> None:
+        seq = np.ascontiguousarray(seq, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        assert offs.size == lens.size
+        _ck(lib().vc_count_block(self._h, _ptr(seq), seq.size, _ptr(offs), _ptr(lens), offs.size),
+            "vc_count_block")
+
+    def count_device(self, seq_ptr: int, seq_bytes: int, offs_ptr: int, lens_ptr: int,
+                     n_reads: int, stream: int = 0) -> None:
+        _ck(lib().vc_count_device(self._h, P(seq_ptr), seq_bytes, P(offs_ptr), P(lens_ptr),
+                                  n_reads, P(stream) if stream else None), "vc_count_device")
+
+    def count_file(self, fn: str, block_size: int = 10_000_000, n_thread: int = 4) -> FileStats:
+        st = FileStats()
+        rc = lib().vc_count_file(self._h, fn.encode(), block_size, n_thread, C.byref(st))
+        if rc == VC_EIO:
+            raise FileNotFoundError(fn)
+        _ck(rc, "vc_count_file(%s)" % fn)
+        return st
+
+    def finish(self):
+        """(counts uint32[2n], kmers_extracted) after all queued work."""
+        counts = np.zeros(2 * self.n_patterns + 2, dtype=np.uint32)
+        km = C.c_uint64()
+        _ck(lib().vc_finish(self._h, _ptr(counts), C.byref(km)), "vc_finish")
+        return counts[:2 * self.n_patterns], km.value
+
+    def reset(self) -> None:
+        _ck(lib().vc_reset(self._h), "vc_reset")
+
+    def bind_outputs(self, counts_ptr: int = 0, tally_ptr: int = 0) -> None:
+        _ck(lib().vc_bind_outputs(self._h, P(counts_ptr) if counts_ptr else None,
+                                  P(tally_ptr) if tally_ptr else None), "vc_bind_outputs")
+
+    @property
+    def stream(self) -> int:
+        return lib().vc_stream(self._h) or 0
+
+    def set_timing(self, on: bool = True) -> None:
+        _ck(lib().vc_set_timing(self._h, 1 if on else 0), "vc_set_timing")
+
+    def kernel_ms(self) -> float:
+        ms = C.c_float()
+        _ck(lib().vc_kernel_ms(self._h, C.byref(ms)), "vc_kernel_ms")
+        return ms.value
+
+    def table_info(self):
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _ck(lib().vc_table_info(self._h, C.byref(a), C.byref(b), C.byref(c)), "vc_table_info")
+        return {"n_keys": a.value, "slots": b.value, "filter_bytes": c.value}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().vc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def create_combined_kmer_map(db: PatternDB, k: int, device: int = 0) -> KmerMap:
+    """create_combined_kmer_map (vaf-counter.c:198): keys -> static device table."""
+    keys, vals, coll = db.keys(k)
+    if coll > 0:
+        sys.stderr.write("[W::create_combined_kmer_map] Warning: %d k-mer collisions detected. "
+                         "Some patterns may have overlapping k-mers.\n" % coll)
+    m = KmerMap(k, keys, vals, db.n, device)
+    m.n_collisions = coll
+    return m
+
+
+def count_fastq_kmers(fn: str, k: int, n_thread: int, block_size: int, kmer_map: KmerMap,
+                      db: PatternDB = None):
+    """count_fastq_kmers (vaf-counter.c:550): silently skips an unopenable file."""
+    assert k == kmer_map.k
+    try:
+        return kmer_map.count_file(fn, block_size, n_thread)
+    except FileNotFoundError:
+        return None
+
+
+def synth_reads(seq_ptr, offs_ptr, lens_ptr, first, n_reads, read_len, seed, f_snp,
+                windows_ptr, dosage_ptr, n_snp, stream=0) -> None:
+    """vafc_synth.gen_reads evaluated on the device (bench / tests)."""
+    _ck(lib().vc_synth_reads(P(seq_ptr), P(offs_ptr), P(lens_ptr), first, n_reads, read_len, seed,
+                             f_snp, P(windows_ptr) if n_snp else None,
+                             P(dosage_ptr) if n_snp else None, n_snp,
+                             P(stream) if stream else None), "vc_synth_reads")
+
+
+def debug_decode(seq_ptr, seq_bytes, offs_ptr, lens_ptr, n_reads, codes_ptr, stream=0) -> None:
+    _ck(lib().vc_debug_decode(P(seq_ptr), seq_bytes, P(offs_ptr), P(lens_ptr), n_reads,
+                              P(codes_ptr), P(stream) if stream else None), "vc_debug_decode")
+
+
+# --------------------------------------------------------------------------
+# CLI mirror (vaf-counter.c:584-738)
+# --------------------------------------------------------------------------
+
+USAGE = (
+    "Usage: vaf-counter [options] -p <patterns.txt> -o <output.vaf> <reads.fq> [reads2.fq ...]\n"
+    "Options:\n"
+    "  -k INT    k-mer length [%d]\n"
+    "  -p FILE   input pattern file\n"
+    "  -o FILE   output VAF file\n"
+    "  -t INT    number of threads [%d]\n"
+    "  -b INT    block size [%d]\n"
+    "  -v        verbose mode (report performance statistics)\n")
+
+
+def parse_args(argv):
+    """ketopt(..., permute=1, "k:p:o:t:b:v") semantics: options may follow files."""
+    opt = {"k": 21, "t": 4, "b": 10_000_000, "p": None, "o": None, "v": False}
+    files, i = [], 0
+    while i < len(argv):
+        a = argv[i]
+        if a == "--":
+            files.extend(argv[i + 1:])
+            break
+        if len(a) >= 2 and a[0] == "-":
+            j = 1
+            while j < len(a):
+                c = a[j]
+                if c in "kpotb":
+                    val = a[j + 1:] if j + 1 < len(a) else (argv[i + 1] if i + 1 < len(argv) else None)
+                    if j + 1 >= len(a):
+                        i += 1
+                    if val is not None:
+                        if c in "ktb":
+                            try:
+                                opt[c] = int(val)
+                            except ValueError:
+                                opt[c] = 0
+                        else:
+                            opt[c] = val
+                    break
+                if c == "v":
+                    opt["v"] = True
+                j += 1
+        else:
+            files.append(a)
+        i += 1
+    return opt, files
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    o, files = parse_args(argv)
+    k = o["k"]
+    if not o["p"] or not o["o"] or not files:
+        sys.stderr.write(USAGE % (k, o["t"], o["b"]))
+        return 1
+    err = sys.stderr.write
+    t_start = time.time()
+    err("[M::main] Loading patterns...\n")
+    t = time.time()
+    try:
+        db = load_patterns(o["p"])
+    except VafcError:
+        err("Error: failed to load pattern file\n")
+        return 1
+    err("[M::main] Loaded %d patterns in %.3f sec\n" % (db.n, time.time() - t))
+    err("[M::main] Creating k-mer map...\n")
+    try:
+        kmap = create_combined_kmer_map(db, k, int(os.environ.get("VAFC_DEVICE", "0")))
+    except VafcError:
+        err("Error: failed to create k-mer map\n")
+        return 1
+    err("[M::main] Counting k-mers in FASTQ files with %d threads...\n" % o["t"])
+    t = time.time()
+    bases = seqs = 0
+    for fn in files:
+        err("[M::main] Processing %s...\n" % fn)
+        st = count_fastq_kmers(fn, k, o["t"], o["b"], kmap, db)
+        if st is not None:
+            bases += st.bases
+            seqs += st.seqs
+    counts, kmers = kmap.finish()
+    t_count = time.time() - t
+    tot = int(counts.astype(np.uint64).sum())
+    avg = tot / (db.n if db.n > 0 else 1)
+    err("[M::main] Writing VAF file...\n")
+    try:
+        db.write_vaf(counts, o["o"])
+    except VafcError:
+        err("Error: failed to open output file\n")
+        return 1
+    err("[M::main] Done. Average depth: %.2f\n" % avg)
+    if o["v"]:
+        err("  Bases processed:       %d (%.2f Mbases)\n" % (bases, bases / 1e6))
+        err("  K-mers extracted:      %d (%.2f million)\n" % (kmers, kmers / 1e6))
+        if t_count > 0:
+            err("  Speed:                 %.2f Mbases/sec\n" % (bases / t_count / 1e6))
+        err("  Total runtime:         %.3f sec\n" % (time.time() - t_start))
+    kmap.close()
+    db.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
