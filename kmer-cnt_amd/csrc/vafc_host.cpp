@@ -229,8 +229,8 @@ struct vc_ctx {
 	uint64_t n_keys = 0;
 	hipStream_t st = nullptr;
 	int n_cu = 256;
-	uint64_t *d_tkeys = nullptr;
-	uint32_t *d_tvals = nullptr;
+	vc_slot_t *d_table = nullptr;
+	int filter_w = VC_FILTER_W64;
 	uint32_t tbits = 0;
 	uint32_t *d_filter = nullptr;
 	uint32_t wbits = 0;
@@ -280,13 +280,15 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
 		c->n_cu = prop.multiProcessorCount;
 
-	// exact table: linear probing, load <= 1/2
+	// exact table: 16-byte {key, value} slots, linear probing, load <= 1/2
 	uint32_t tbits = 4;
 	while (((uint64_t)1 << tbits) < 2 * (uint64_t)n_keys + 2) ++tbits;
 	const uint64_t tslots = (uint64_t)1 << tbits;
-	std::vector<uint64_t> tk(tslots, VC_EMPTY_KEY);
-	std::vector<uint32_t> tv(tslots, 0);
-	// prefilter: >= 24 bits per key, 1 KiB .. 128 KiB
+	std::vector<vc_slot_t> tab(tslots, vc_slot_t{VC_EMPTY_KEY, 0u, 0u});
+	// LDS prefilter: >= 24 bits per key, 1 KiB .. 128 KiB; 64-bit words with
+	// 4 bits per key (default) or 32-bit words with 2 bits (VAFC_FILTER=32)
+	const char *fenv = getenv("VAFC_FILTER");
+	const int filter_w = (fenv && atoi(fenv) == 32) ? VC_FILTER_W32 : VC_FILTER_W64;
 	uint32_t wbits = 8;
 	while (wbits < VC_MAX_FILTER_WBITS && ((uint64_t)32 << wbits) < 24 * (uint64_t)n_keys) ++wbits;
 	std::vector<uint32_t> fw((size_t)1 << wbits, 0);
@@ -297,19 +299,27 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 		const uint32_t h = vc_hash(key);
 		uint32_t s = vc_table_slot(h, tbits);
 		bool dup = false;
-		while (tk[s] != VC_EMPTY_KEY) {
-			if (tk[s] == key) { dup = true; break; }
+		while (tab[s].key != VC_EMPTY_KEY) {
+			if (tab[s].key == key) { dup = true; break; }
 			s = (s + 1) & (uint32_t)(tslots - 1);
 		}
 		if (dup) continue;             // first occurrence wins
-		tk[s] = key;
-		tv[s] = vals[i];
-		fw[vc_filter_word(h, wbits)] |= vc_filter_mask(h, wbits);
+		tab[s].key = key;
+		tab[s].val = vals[i];
+		const uint32_t fx = vc_filter_hash(key, k);
+		if (filter_w == VC_FILTER_W32) {
+			fw[vc_filter_word(fx, wbits)] |= vc_filter_mask(fx);
+		} else {
+			const uint32_t w = vc_filter_word(fx, wbits - 1);
+			fw[2 * w] |= vc_filter_mask_lo(fx);
+			fw[2 * w + 1] |= vc_filter_mask_hi(fx, vc_filter_hash2(key, k));
+		}
 		++inserted;
 	}
 	c->n_keys = inserted;
 	c->tbits = tbits;
 	c->wbits = wbits;
+	c->filter_w = filter_w;
 
 	int rc = VC_OK;
 #define TRY(call)                                                                        \
@@ -322,16 +332,14 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 		}                                                                                \
 	} while (0)
 	TRY(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-	TRY(hipMalloc(&c->d_tkeys, tslots * sizeof(uint64_t)));
-	TRY(hipMalloc(&c->d_tvals, tslots * sizeof(uint32_t)));
+	TRY(hipMalloc(&c->d_table, tslots * sizeof(vc_slot_t)));
 	TRY(hipMalloc(&c->d_filter, fw.size() * sizeof(uint32_t)));
 	TRY(hipMalloc(&c->own_counts, (2 * (size_t)n_patterns + 2) * sizeof(uint32_t)));
 	TRY(hipMalloc(&c->own_tally, sizeof(unsigned long long)));
 	c->d_counts = c->own_counts;
 	c->d_tally = c->own_tally;
 	TRY(hipMalloc(&c->d_nlong, sizeof(uint32_t)));
-	TRY(hipMemcpy(c->d_tkeys, tk.data(), tslots * sizeof(uint64_t), hipMemcpyHostToDevice));
-	TRY(hipMemcpy(c->d_tvals, tv.data(), tslots * sizeof(uint32_t), hipMemcpyHostToDevice));
+	TRY(hipMemcpy(c->d_table, tab.data(), tslots * sizeof(vc_slot_t), hipMemcpyHostToDevice));
 	TRY(hipMemcpy(c->d_filter, fw.data(), fw.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
 	TRY(hipMemset(c->d_counts, 0, (2 * (size_t)n_patterns + 2) * sizeof(uint32_t)));
 	TRY(hipMemset(c->d_tally, 0, sizeof(unsigned long long)));
@@ -376,8 +384,7 @@ extern "C" void vc_destroy(vc_ctx *c)
 	}
 	if (c->t0) (void)hipEventDestroy(c->t0);
 	if (c->t1) (void)hipEventDestroy(c->t1);
-	if (c->d_tkeys) (void)hipFree(c->d_tkeys);
-	if (c->d_tvals) (void)hipFree(c->d_tvals);
+	if (c->d_table) (void)hipFree(c->d_table);
 	if (c->d_filter) (void)hipFree(c->d_filter);
 	if (c->own_counts) (void)hipFree(c->own_counts);
 	if (c->own_tally) (void)hipFree(c->own_tally);
@@ -402,12 +409,12 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 	A.offs = d_offs;
 	A.lens = d_lens;
 	A.n_reads = n_reads;
-	A.tkeys = c->d_tkeys;
-	A.tvals = c->d_tvals;
+	A.table = c->d_table;
 	A.tbits = c->tbits;
 	A.tmask = (uint32_t)(((uint64_t)1 << c->tbits) - 1);
 	A.filter = c->d_filter;
 	A.wbits = c->wbits;
+	A.filter_w = c->filter_w;
 	A.k = c->k;
 	A.kmask = ((uint64_t)1 << (2 * c->k)) - 1;
 	A.counts = c->d_counts;

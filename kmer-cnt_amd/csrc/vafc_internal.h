@@ -8,6 +8,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "vafc_common.h"
+
 #define VC_BLOCK 1024        // threads per block: 16 waves, one block per CU
 #define VC_QCAP 128          // per-wave LDS queue entries
 
@@ -18,11 +20,11 @@ struct VcKernelArgs {
 	const uint64_t *offs;
 	const uint32_t *lens;
 	uint64_t n_reads;
-	const uint64_t *tkeys;       // exact table, 2^tbits slots, VC_EMPTY_KEY = empty
-	const uint32_t *tvals;
+	const vc_slot_t *table;      // exact table, 2^tbits slots, key VC_EMPTY_KEY = empty
 	uint32_t tbits, tmask;
-	const uint32_t *filter;      // 2^wbits words
+	const uint32_t *filter;      // 2^wbits 32-bit words (2^(wbits-1) 64-bit words)
 	uint32_t wbits;
+	int filter_w;                // VC_FILTER_W32 or VC_FILTER_W64
 	int k;
 	uint64_t kmask;              // (1 << 2k) - 1
 	uint32_t *counts;            // [2 * n_patterns]
@@ -32,9 +34,11 @@ struct VcKernelArgs {
 	uint32_t long_cap;
 };
 
+// LDS: prefilter words + 4 zero words (16-byte aligned), then the per-wave queues.
+__host__ __device__ static inline uint32_t vc_filter_lds_words(uint32_t wbits) { return (1u << wbits) + 4u; }
 static inline size_t vc_lds_bytes(uint32_t wbits)
 {
-	return ((size_t)4 << wbits) + (size_t)(VC_BLOCK / 64) * VC_QCAP * 8;
+	return (size_t)4 * vc_filter_lds_words(wbits) + (size_t)(VC_BLOCK / 64) * VC_QCAP * 8;
 }
 
 #ifdef __cplusplus

@@ -32,7 +32,6 @@
 #include "vafc_internal.h"
 
 #define WAVE 64
-#define QCAP 128            // per-wave LDS queue entries (u64)
 
 // ---------------------------------------------------------------------------
 // small helpers
@@ -105,18 +104,46 @@ __device__ __forceinline__ uint32_t ldw(const uint32_t *__restrict__ s32, uint64
 	return s32[i < wmax ? i : wmax];
 }
 
+// Four consecutive dwords from a 4-byte-aligned index: one global_load_dwordx4
+// when all four are inside the buffer, else four clamped dword loads (the
+// last reads of a batch).  Loaded bytes past a read's end are masked later.
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ void ld4(const uint32_t *__restrict__ s32, uint64_t i, uint64_t wmax,
+                                    uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
+{
+	if (i + 3 <= wmax) {
+		const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(s32 + i);
+		a = v.x; b = v.y; c = v.z; d = v.w;
+	} else {
+		a = ldw(s32, i, wmax); b = ldw(s32, i + 1, wmax); c = ldw(s32, i + 2, wmax); d = ldw(s32, i + 3, wmax);
+	}
+}
+
 // ---------------------------------------------------------------------------
 // exact table probe (drain side)
 // ---------------------------------------------------------------------------
 
-__device__ __forceinline__ void probe_and_count(const VcKernelArgs &A, uint64_t key)
+// Reverse complement of a right-aligned k-mer with bit tricks (drain side only).
+__device__ __forceinline__ uint64_t revcomp_dev(uint64_t x, int k)
 {
-	uint32_t h = vc_hash(key);
-	uint32_t s = vc_table_slot(h, A.tbits);
+	const uint32_t lo = __builtin_bitreverse32((uint32_t)x), hi = __builtin_bitreverse32((uint32_t)(x >> 32));
+	uint64_t r = ((uint64_t)lo << 32) | hi;                                  // bit-reversed
+	r = ((r >> 1) & 0x5555555555555555ull) | ((r & 0x5555555555555555ull) << 1); // restore 2-bit order
+	return (~r) >> (64 - 2 * k);
+}
+
+// key: the raw forward k-mer (bits above 2k may hold older bases).
+__device__ __forceinline__ void probe_and_count(const VcKernelArgs &A, uint64_t fwd_raw)
+{
+	const uint64_t f = fwd_raw & A.kmask;
+	const uint64_t r = revcomp_dev(f, A.k);
+	const uint64_t key = f < r ? f : r;
+	uint32_t s = vc_table_slot(vc_hash(key), A.tbits);
 	for (;;) {
-		uint64_t k2 = A.tkeys[s];
+		const uint4 e = *reinterpret_cast<const uint4 *>(&A.table[s]);
+		const uint64_t k2 = ((uint64_t)e.y << 32) | e.x;
 		if (k2 == key) {
-			atomicAdd(&A.counts[A.tvals[s]], 1u);
+			atomicAdd(&A.counts[e.z], 1u);
 			break;
 		}
 		if (k2 == VC_EMPTY_KEY) break;
@@ -125,29 +152,28 @@ __device__ __forceinline__ void probe_and_count(const VcKernelArgs &A, uint64_t 
 }
 
 struct WaveQueue {
-	uint64_t *q;     // LDS, QCAP entries
+	uint64_t *q;     // LDS, VC_QCAP entries
 	uint32_t n;      // wave-uniform fill
 };
 
-__device__ __forceinline__ void queue_push(const VcKernelArgs &A, WaveQueue &Q, bool hit,
-                                           uint64_t key, int lane)
+// Lanes with `hit` append `key` (bal = ballot(hit) != 0); a queue holding a
+// full wave's worth is drained by all 64 lanes probing the table at once.
+__device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q, uint64_t bal,
+                                             bool hit, uint64_t key, int lane)
 {
-	uint64_t bal = __ballot(hit);
-	if (bal) {
-		uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-		                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-		if (hit) Q.q[Q.n + pre] = key;
-		Q.n += (uint32_t)__popcll(bal);
-		if (Q.n >= WAVE) {
-			__builtin_amdgcn_wave_barrier();
-			uint64_t k0 = Q.q[lane];
-			uint32_t rest = Q.n - WAVE;
-			uint64_t k1 = Q.q[lane + WAVE];
-			__builtin_amdgcn_wave_barrier();
-			if ((uint32_t)lane < rest) Q.q[lane] = k1;
-			Q.n = rest;
-			probe_and_count(A, k0);
-		}
+	const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+	                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+	if (hit) Q.q[Q.n + pre] = key;
+	Q.n = __builtin_amdgcn_readfirstlane(Q.n + (uint32_t)__popcll(bal));
+	if (Q.n >= WAVE) {
+		__builtin_amdgcn_wave_barrier();
+		const uint64_t k0 = Q.q[lane];
+		const uint32_t rest = Q.n - WAVE;
+		const uint64_t k1 = Q.q[lane + WAVE];
+		__builtin_amdgcn_wave_barrier();
+		if ((uint32_t)lane < rest) Q.q[lane] = k1;
+		Q.n = rest;
+		probe_and_count(A, k0);
 	}
 }
 
@@ -159,86 +185,161 @@ __device__ __forceinline__ void queue_flush(const VcKernelArgs &A, WaveQueue &Q,
 }
 
 // ---------------------------------------------------------------------------
+// rolling forward / reverse-complement k-mers (vaf-counter.c:368-394)
+// ---------------------------------------------------------------------------
+//
+// K > 0: compile-time k, k-mers held as 32-bit halves and rolled with
+// v_alignbit / v_lshl_or; K == 0: run-time k on 64-bit values.  Instead of
+// resetting on an invalid base (the reference's `l = 0; x = 0`), a 32-bit
+// register of invalid flags is shifted right with v_alignbit (newest flag in
+// bit 31): the window is valid iff its top k bits are zero, i.e. the register
+// is below 2^(32-k).  fwd/rev hold exactly the last k codes once it is.
+template <int K>
+struct Roller {
+	uint32_t flo, fhi, rlo, rhi, inv;
+	uint32_t vthr;        // valid <=> inv < vthr
+	uint64_t kmask;
+	uint32_t rsh;
+
+	__device__ __forceinline__ void init(const VcKernelArgs &A)
+	{
+		flo = fhi = rlo = rhi = 0;
+		inv = 0xFFFFFFFFu;
+		const int k = K ? K : A.k;
+		vthr = 1u << (32 - k);
+		kmask = A.kmask;
+		rsh = 2u * (uint32_t)(k - 1);
+	}
+	// c: 2-bit code, bad: bit 0 = invalid flag (higher bits ignored)
+	__device__ __forceinline__ void push(uint32_t c, uint32_t bad)
+	{
+		const uint32_t cc = c ^ 3u;
+		if constexpr (K >= 17) {
+			constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
+			fhi = __builtin_amdgcn_alignbit(fhi, flo, 30) & HIM;
+			flo = (flo << 2) | c;
+			rlo = __builtin_amdgcn_alignbit(rhi, rlo, 2);
+			rhi = (rhi >> 2) | (cc << (2 * K - 34));
+		} else if constexpr (K > 0) {
+			constexpr uint32_t M = K == 16 ? 0xFFFFFFFFu : ((1u << (2 * K)) - 1u);
+			flo = ((flo << 2) | c) & M;
+			rlo = (rlo >> 2) | (cc << (2 * K - 2));
+		} else {
+			uint64_t f = ((((uint64_t)fhi << 32) | flo) << 2 | c) & kmask;
+			uint64_t r = ((((uint64_t)rhi << 32) | rlo) >> 2) | ((uint64_t)cc << rsh);
+			flo = (uint32_t)f; fhi = (uint32_t)(f >> 32);
+			rlo = (uint32_t)r; rhi = (uint32_t)(r >> 32);
+		}
+		inv = __builtin_amdgcn_alignbit(bad, inv, 1);
+	}
+	__device__ __forceinline__ bool valid() const { return inv < vthr; }
+	// prefilter hash: symmetric in the strands, so no min() per k-mer
+	__device__ __forceinline__ uint32_t fx() const { return flo + rlo; }
+};
+
+__device__ __forceinline__ uint64_t canonical_of(uint32_t flo, uint32_t fhi, uint32_t rlo, uint32_t rhi)
+{
+	const uint64_t f = ((uint64_t)fhi << 32) | flo, r = ((uint64_t)rhi << 32) | rlo;
+	return f < r ? f : r;
+}
+
+// ---------------------------------------------------------------------------
 // scan one span of one read per lane, wave-uniform trip count
 // ---------------------------------------------------------------------------
 //
 // Lane processes chunks [c_lo, c_hi) of its read (chunk c = read positions
 // 16c..16c+15), emitting the canonical k-mers whose whole window lies in the
 // valid position range [vlo, vhi) (vlo = 0, vhi = len for a whole read).
-template <bool HAS_LO>
+// Returns nothing; the wave's count of valid k-mers accumulates in `tally`
+// (wave-uniform).
+template <int K, bool W64, bool HAS_LO>
 __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
                                           uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
                                           int vlo, int vhi, int nit, const uint32_t *__restrict__ filt,
                                           WaveQueue &Q, uint32_t &tally, int lane)
 {
-	const int k = A.k;
-	const uint64_t kmask = A.kmask;
-	const uint32_t rsh = 2u * (uint32_t)(k - 1);
-	const uint32_t kshl = 32u - (uint32_t)k;
-	const uint32_t wsh = 32u - A.wbits, b1s = 27u - A.wbits, b2s = 22u - A.wbits;
+	const uint32_t wbits = A.wbits;
+	const uint32_t zero_word = 1u << wbits;     // an all-zero LDS word past the filter
 	const int tail_c = (len & 15) ? (len >> 4) : -1;
 
 	uint64_t addr = off + 16ull * (uint64_t)c_lo;
 	uint64_t wi = addr >> 2;
-	uint32_t sh = (uint32_t)(addr & 3u);
-	bool act = c_lo < c_hi;
+	const uint32_t sh = (uint32_t)(addr & 3u);
 	uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
-	if (act) {
-		w0 = ldw(s32, wi, wmax); w1 = ldw(s32, wi + 1, wmax); w2 = ldw(s32, wi + 2, wmax);
-		w3 = ldw(s32, wi + 3, wmax); w4 = ldw(s32, wi + 4, wmax);
+	if (c_lo < c_hi) {
+		ld4(s32, wi, wmax, w0, w1, w2, w3);
+		w4 = ldw(s32, wi + 4, wmax);
 	}
-	uint64_t fwd = 0, rev = 0;
-	uint32_t inv = 0xFFFFFFFFu;
+	Roller<K> R;
+	R.init(A);
 
 	for (int it = 0; it < nit; ++it) {
 		const int c = c_lo + it;
-		act = c < c_hi;
-		// next chunk's words (w4 becomes the next w0)
+		// next chunk's dwords are in flight while this chunk is processed
 		uint32_t x1 = 0, x2 = 0, x3 = 0, x4 = 0;
-		if (c + 1 < c_hi) {
-			x1 = ldw(s32, wi + 5, wmax); x2 = ldw(s32, wi + 6, wmax);
-			x3 = ldw(s32, wi + 7, wmax); x4 = ldw(s32, wi + 8, wmax);
-		}
-		uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
-		uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
-		uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
-		uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
-		uint32_t t0, t1, t2, t3;
-		if (c == tail_c) {
-			t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3);
-		} else {
-			t0 = dec_head(b0); t1 = dec_head(b1); t2 = dec_head(b2); t3 = dec_head(b3);
+		if (c + 1 < c_hi) ld4(s32, wi + 5, wmax, x1, x2, x3, x4);
+		const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+		const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+		const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+		const uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
+		uint32_t t0 = dec_head(b0), t1 = dec_head(b1), t2 = dec_head(b2), t3 = dec_head(b3);
+		if (__ballot(c == tail_c)) {
+			if (c == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
 		}
 		const int P = 16 * c;
-		t0 |= range_mask_hi(vhi - P);
-		t1 |= range_mask_hi(vhi - P - 4);
-		t2 |= range_mask_hi(vhi - P - 8);
-		t3 |= range_mask_hi(vhi - P - 12);
-		if (HAS_LO) {
-			t0 |= range_mask_lo(vlo - P);
-			t1 |= range_mask_lo(vlo - P - 4);
-			t2 |= range_mask_lo(vlo - P - 8);
-			t3 |= range_mask_lo(vlo - P - 12);
+		if (__ballot(P + 16 > vhi)) {   // past the span end (and inactive lanes: P >= vhi)
+			t0 |= range_mask_hi(vhi - P);
+			t1 |= range_mask_hi(vhi - P - 4);
+			t2 |= range_mask_hi(vhi - P - 8);
+			t3 |= range_mask_hi(vhi - P - 12);
 		}
-		if (!act) { t0 = t1 = t2 = t3 = 0x04040404u; }
+		if (HAS_LO) {
+			if (__ballot(P < vlo)) {
+				t0 |= range_mask_lo(vlo - P);
+				t1 |= range_mask_lo(vlo - P - 4);
+				t2 |= range_mask_lo(vlo - P - 8);
+				t3 |= range_mask_lo(vlo - P - 12);
+			}
+		}
 
 #pragma unroll
-		for (int j = 0; j < 16; ++j) {
-			const uint32_t tw = j < 4 ? t0 : (j < 8 ? t1 : (j < 12 ? t2 : t3));
-			const uint32_t x = tw >> (8 * (j & 3));
-			const uint32_t cb = x & 3u;
-			const uint32_t bad = (x >> 2) & 1u;
-			fwd = ((fwd << 2) | cb) & kmask;
-			rev = (rev >> 2) | ((uint64_t)(cb ^ 3u) << rsh);
-			inv = (inv << 1) | bad;
-			const bool valid = (inv << kshl) == 0u;
-			const uint64_t can = fwd < rev ? fwd : rev;
-			const uint32_t h = vc_hash(can);
-			const uint32_t fw = filt[h >> wsh];
-			const uint32_t fm = (1u << ((h >> b1s) & 31u)) | (1u << ((h >> b2s) & 31u));
-			const bool hit = valid && ((fw & fm) == fm);
-			tally += valid ? 1u : 0u;
-			queue_push(A, Q, hit, can, lane);
+		for (int half = 0; half < 2; ++half) {
+			const uint32_t ta = half ? t2 : t0, tb = half ? t3 : t1;
+			uint32_t fl[8], fh[8], fw[8], fw2[8], fxs[8], fys[8];
+#pragma unroll
+			for (int j = 0; j < 8; ++j) {
+				const uint32_t tw = j < 4 ? ta : tb;
+				const uint32_t x = tw >> (8 * (j & 3));
+				R.push(x & 3u, x >> 2);
+				const bool valid = R.valid();
+				tally += valid ? 1u : 0u;
+				const uint32_t fx = R.fx();
+				if constexpr (W64) {
+					const uint32_t widx = valid ? vc_filter_word(fx, wbits - 1u) : (zero_word >> 1);
+					const uint2 w = reinterpret_cast<const uint2 *>(filt)[widx];
+					fw[j] = w.x;
+					fw2[j] = w.y;
+					fys[j] = R.flo ^ R.rlo;
+				} else {
+					const uint32_t widx = valid ? vc_filter_word(fx, wbits) : zero_word;
+					fw[j] = filt[widx];
+				}
+				fxs[j] = fx;
+				fl[j] = R.flo; fh[j] = R.fhi;
+			}
+#pragma unroll
+			for (int j = 0; j < 8; ++j) {
+				bool hit;
+				if constexpr (W64) {
+					const uint32_t ml = vc_filter_mask_lo(fxs[j]), mh = vc_filter_mask_hi(fxs[j], fys[j]);
+					hit = (((fw[j] & ml) ^ ml) | ((fw2[j] & mh) ^ mh)) == 0u;
+				} else {
+					const uint32_t fm = vc_filter_mask(fxs[j]);
+					hit = (fw[j] & fm) == fm;
+				}
+				const uint64_t bal = __ballot(hit);
+				if (bal) queue_append(A, Q, bal, hit, ((uint64_t)fh[j] << 32) | fl[j], lane);
+			}
 		}
 		w0 = w4; w1 = x1; w2 = x2; w3 = x3; w4 = x4;
 		wi += 4;
@@ -251,6 +352,7 @@ __device__ __forceinline__ void load_filter(const VcKernelArgs &A, uint32_t *fil
 	const uint4 *src = reinterpret_cast<const uint4 *>(A.filter);
 	uint4 *dst = reinterpret_cast<uint4 *>(filt);
 	for (uint32_t i = threadIdx.x; i < nw / 4u; i += blockDim.x) dst[i] = src[i];
+	if (threadIdx.x < 4) filt[nw + threadIdx.x] = 0u;     // the zero word(s)
 	__syncthreads();
 }
 
@@ -258,6 +360,7 @@ __device__ __forceinline__ void load_filter(const VcKernelArgs &A, uint32_t *fil
 // kernel 1: whole reads, one lane per read
 // ---------------------------------------------------------------------------
 
+template <int K, bool W64>
 __global__ void __launch_bounds__(VC_BLOCK)
 vc_count_reads_kernel(VcKernelArgs A)
 {
@@ -266,13 +369,13 @@ vc_count_reads_kernel(VcKernelArgs A)
 	const int lane = threadIdx.x & (WAVE - 1);
 	const int wave = threadIdx.x / WAVE;
 	WaveQueue Q;
-	Q.q = reinterpret_cast<uint64_t *>(smem + (1u << A.wbits)) + wave * QCAP;
+	Q.q = reinterpret_cast<uint64_t *>(smem + vc_filter_lds_words(A.wbits)) + wave * VC_QCAP;
 	Q.n = 0;
 	load_filter(A, filt);
 
 	const uint32_t *s32 = reinterpret_cast<const uint32_t *>(A.seq);
 	const uint64_t wmax = A.seq_words ? A.seq_words - 1 : 0;
-	unsigned long long tally_all = 0;
+	uint32_t tally = 0;
 
 	for (uint64_t g = blockIdx.x; g * (uint64_t)VC_BLOCK < A.n_reads; g += gridDim.x) {
 		const uint64_t r = g * (uint64_t)VC_BLOCK + threadIdx.x;
@@ -289,19 +392,18 @@ vc_count_reads_kernel(VcKernelArgs A)
 		}
 		const int nch = (len + 15) >> 4;
 		const int nit = wave_max_i32(nch);
-		uint32_t tally = 0;
-		scan_span<false>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tally, lane);
-		tally_all += tally;
+		scan_span<K, W64, false>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tally, lane);
 	}
 	queue_flush(A, Q, lane);
-	tally_all = wave_sum_u64(tally_all);
-	if (lane == 0 && tally_all) atomicAdd(A.tally, tally_all);
+	const unsigned long long t = wave_sum_u64(tally);
+	if (lane == 0 && t) atomicAdd(A.tally, t);
 }
 
 // ---------------------------------------------------------------------------
 // kernel 2: long reads, every lane of the grid takes one segment
 // ---------------------------------------------------------------------------
 
+template <int K, bool W64>
 __global__ void __launch_bounds__(VC_BLOCK)
 vc_count_long_kernel(VcKernelArgs A)
 {
@@ -313,14 +415,14 @@ vc_count_long_kernel(VcKernelArgs A)
 	const int lane = threadIdx.x & (WAVE - 1);
 	const int wave = threadIdx.x / WAVE;
 	WaveQueue Q;
-	Q.q = reinterpret_cast<uint64_t *>(smem + (1u << A.wbits)) + wave * QCAP;
+	Q.q = reinterpret_cast<uint64_t *>(smem + vc_filter_lds_words(A.wbits)) + wave * VC_QCAP;
 	Q.n = 0;
 	load_filter(A, filt);
 
 	const uint32_t *s32 = reinterpret_cast<const uint32_t *>(A.seq);
 	const uint64_t wmax = A.seq_words ? A.seq_words - 1 : 0;
-	const int k = A.k;
-	unsigned long long tally_all = 0;
+	const int k = K ? K : A.k;
+	uint32_t tally = 0;
 	const uint64_t stride = (uint64_t)gridDim.x * VC_BLOCK;
 
 	for (uint32_t li = 0; li < nl; ++li) {
@@ -340,14 +442,12 @@ vc_count_long_kernel(VcKernelArgs A)
 				c_hi = (vhi + 15) >> 4;
 			}
 			const int nit = wave_max_i32(c_hi - c_lo);
-			uint32_t tally = 0;
-			scan_span<true>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tally, lane);
-			tally_all += tally;
+			scan_span<K, W64, true>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tally, lane);
 		}
 	}
 	queue_flush(A, Q, lane);
-	tally_all = wave_sum_u64(tally_all);
-	if (lane == 0 && tally_all) atomicAdd(A.tally, tally_all);
+	const unsigned long long t = wave_sum_u64(tally);
+	if (lane == 0 && t) atomicAdd(A.tally, t);
 }
 
 // ---------------------------------------------------------------------------
@@ -442,24 +542,57 @@ __global__ void vc_synth_kernel(uint8_t *seq, uint64_t *offs, uint32_t *lens, ui
 // launchers
 // ---------------------------------------------------------------------------
 
-extern "C" hipError_t vc_launch_count(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
+template <int K, bool W64>
+static hipError_t launch_kw(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
 {
 	const size_t lds = vc_lds_bytes(A->wbits);
-	hipLaunchKernelGGL(vc_count_reads_kernel, dim3(grid), dim3(VC_BLOCK), lds, st, *A);
+	hipLaunchKernelGGL((vc_count_reads_kernel<K, W64>), dim3(grid), dim3(VC_BLOCK), lds, st, *A);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return e;
-	hipLaunchKernelGGL(vc_count_long_kernel, dim3(grid_long), dim3(VC_BLOCK), lds, st, *A);
+	hipLaunchKernelGGL((vc_count_long_kernel<K, W64>), dim3(grid_long), dim3(VC_BLOCK), lds, st, *A);
 	return hipGetLastError();
+}
+
+template <int K>
+static hipError_t launch_k(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
+{
+	return A->filter_w == VC_FILTER_W64 ? launch_kw<K, true>(A, grid, grid_long, st)
+	                                    : launch_kw<K, false>(A, grid, grid_long, st);
+}
+
+extern "C" hipError_t vc_launch_count(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
+{
+	switch (A->k) {
+	case 21: return launch_k<21>(A, grid, grid_long, st);
+	case 31: return launch_k<31>(A, grid, grid_long, st);
+	default: return launch_k<0>(A, grid, grid_long, st);
+	}
+}
+
+template <int K, bool W64>
+static hipError_t setup_kw(int lds)
+{
+	hipError_t e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<K, W64>,
+	                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+	if (e != hipSuccess) return e;
+	return hipFuncSetAttribute((const void *)vc_count_long_kernel<K, W64>,
+	                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+template <int K>
+static hipError_t setup_k(int lds)
+{
+	hipError_t e = setup_kw<K, true>(lds);
+	return e == hipSuccess ? setup_kw<K, false>(lds) : e;
 }
 
 extern "C" hipError_t vc_kernel_setup(void)
 {
-	const size_t lds = vc_lds_bytes(VC_MAX_FILTER_WBITS);
-	hipError_t e = hipFuncSetAttribute((const void *)vc_count_reads_kernel,
-	                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-	if (e != hipSuccess) return e;
-	return hipFuncSetAttribute((const void *)vc_count_long_kernel,
-	                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+	const int lds = (int)vc_lds_bytes(VC_MAX_FILTER_WBITS);
+	hipError_t e = setup_k<21>(lds);
+	if (e == hipSuccess) e = setup_k<31>(lds);
+	if (e == hipSuccess) e = setup_k<0>(lds);
+	return e;
 }
 
 extern "C" hipError_t vc_launch_decode(const uint8_t *seq, uint64_t seq_bytes, const uint64_t *offs,

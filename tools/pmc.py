@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Collect rocprofv3 PMC counters for the counting kernel, one pass per group.
+
+Run on the GPU box:  python tools/pmc.py OUTDIR [bench args...]
+Each pass is a separate `rocprofv3 --kernel-trace --pmc ... -- python3 bench.py`
+(no sys/runtime tracing with --pmc).  Writes OUTDIR/pmc_counters.json with the
+per-dispatch average of each counter for vc_count_reads_kernel, plus derived
+numbers (HBM bytes per launch with gfx950's FETCH_SIZE x2 correction).
+"""
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PASSES = [
+    "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES",
+    "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT",
+    "SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM_RD SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 GRBM_GUI_ACTIVE",
+    "FETCH_SIZE",
+    "WRITE_SIZE",
+    "TA_BUSY_avr TA_TA_BUSY_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum",
+    "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum",
+]
+KERNEL = "vc_count_reads_kernel"
+
+
+def main():
+    out = os.path.abspath(sys.argv[1])
+    bench_args = sys.argv[2:] or ["--steps", "2", "--warmup", "1", "--no-cpu"]
+    os.makedirs(out, exist_ok=True)
+    acc = {}
+    for i, group in enumerate(PASSES):
+        d = os.path.join(out, "pass%d" % i)
+        cmd = ["rocprofv3", "--kernel-trace", "--pmc"] + group.split() + [
+            "-d", d, "-o", "p", "--output-format", "csv", "--",
+            "python3", os.path.join(ROOT, "bench.py")] + bench_args
+        r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=900)
+        with open(os.path.join(out, "pass%d.log" % i), "w") as f:
+            f.write(r.stdout[-20000:] + "\n---\n" + r.stderr[-20000:])
+        if r.returncode != 0:
+            print("pass %d failed (rc %d)" % (i, r.returncode), flush=True)
+            continue
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        vals = {}
+        for fn in files:
+            with open(fn) as f:
+                for row in csv.DictReader(f):
+                    if KERNEL not in row.get("Kernel_Name", ""):
+                        continue
+                    key = (row["Counter_Name"])
+                    vals.setdefault(key, {}).setdefault(row.get("Dispatch_Id", "0"), 0.0)
+                    vals[key][row.get("Dispatch_Id", "0")] += float(row["Counter_Value"])
+        for name, per in vals.items():
+            acc[name] = sum(per.values()) / max(len(per), 1)
+        print("pass %d ok: %s" % (i, ", ".join("%s=%.4g" % (n, acc[n]) for n in group.split() if n in acc)),
+              flush=True)
+    derived = {}
+    if "FETCH_SIZE" in acc:
+        derived["hbm_read_bytes_per_launch"] = acc["FETCH_SIZE"] * 1024 * 2   # gfx950: FETCH_SIZE reads 1/2
+    if "WRITE_SIZE" in acc:
+        derived["hbm_write_bytes_per_launch"] = acc["WRITE_SIZE"] * 1024
+    if derived:
+        derived["hbm_bytes_per_launch"] = sum(derived.values())
+    with open(os.path.join(out, "pmc_counters.json"), "w") as f:
+        json.dump({"kernel": KERNEL, "bench_args": bench_args, "counters": acc, "derived": derived}, f, indent=1)
+    print(json.dumps(derived))
+
+
+if __name__ == "__main__":
+    main()
