@@ -158,6 +158,17 @@ typedef struct {
 int vc_count_file(vc_ctx *ctx, const char *path, int block_bases, int n_threads,
                   vc_file_stats *st);
 
+/* Host-only: the same reader + block loop without a device (no counting).
+ * Accepted read bytes / lengths are copied out while they fit (either output
+ * may be NULL).  Lets the reader semantics be checked on machines without a
+ * GPU and measures host ingest speed. */
+int vc_scan_file(const char *path, int k, int block_bases, vc_file_stats *st,
+                 uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out, size_t lens_cap);
+
+/* Host-only: the kseq_read return value of every record until -1 (inclusive),
+ * written while they fit; returns the number of calls made, or VC_EIO. */
+int64_t vc_scan_records(const char *path, int32_t *rets, int64_t cap);
+
 /* ------------------------------------------------------------------ */
 /* Synthetic workload (bench / tests): the generator of vafc_synth.py,  */
 /* evaluated on the device.                                            */

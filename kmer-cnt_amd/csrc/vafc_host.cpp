@@ -640,6 +640,32 @@ double wall_now()
 
 } // namespace
 
+// The reference's per-file block loop.  kt_pipeline(3 workers) runs
+// worker_pipeline's step 0 strictly in block order and each worker retires on
+// the first empty block it reads, so a file ends at its third empty block
+// (kthread.c:97-128, vaf-counter.c:486-517).  Reads shorter than k are
+// skipped and not counted; a -1/-2 from the reader ends the current block.
+template <class Sink>
+static int block_loop(VcFastqReader &rd, int k, int block_bases, Sink &&sink, vc_file_stats &st)
+{
+	int empty = 0, rc = VC_OK;
+	while (empty < 3 && rc == VC_OK) {
+		int64_t sum = 0;
+		int ret;
+		while ((ret = rd.next()) >= 0) {
+			if (ret < k) continue;
+			if ((rc = sink(rd.seq(), (size_t)ret)) != VC_OK) break;
+			sum += ret;
+			st.bases += (uint64_t)ret;
+			st.seqs += 1;
+			if (sum >= block_bases) break;
+		}
+		if (sum == 0) ++empty;
+		else ++st.blocks;
+	}
+	return rc;
+}
+
 extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n_threads,
                              vc_file_stats *st)
 {
@@ -651,30 +677,49 @@ extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n
 	VcFastqReader rd;
 	if (!rd.open(path)) return VC_EIO;
 	BatchWriter bw(c);
-	// kt_pipeline(3 workers) + worker_pipeline step 0: every worker retires
-	// on the first empty block it reads and step 0 runs strictly in block
-	// order, so a file ends at its third empty block (kthread.c:97-128,
-	// vaf-counter.c:486-517).
-	int empty = 0, rc = VC_OK;
-	while (empty < 3 && rc == VC_OK) {
-		int64_t sum = 0;
-		int ret;
-		while ((ret = rd.next()) >= 0) {
-			if (ret < c->k) continue;
-			if ((rc = bw.add(rd.seq(), (size_t)ret)) != VC_OK) break;
-			sum += ret;
-			local.bases += (uint64_t)ret;
-			local.seqs += 1;
-			if (sum >= block_bases) break;
-		}
-		if (sum == 0) ++empty;
-		else ++local.blocks;
-	}
+	int rc = block_loop(rd, c->k, block_bases,
+	                    [&bw](const char *s, size_t l) { return bw.add(s, l); }, local);
 	if (rc == VC_OK) rc = bw.flush();
 	if (rc == VC_OK) HIPCK(hipStreamSynchronize(c->st));
 	local.seconds = wall_now() - t0;
 	if (st) *st = local;
 	return rc;
+}
+
+extern "C" int vc_scan_file(const char *path, int k, int block_bases, vc_file_stats *st,
+                            uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out, size_t lens_cap)
+{
+	if (!path || !st) return VC_EINVAL;
+	vc_file_stats local = {0, 0, 0, 0.0};
+	const double t0 = wall_now();
+	VcFastqReader rd;
+	if (!rd.open(path)) return VC_EIO;
+	size_t nb = 0, nr = 0;
+	int rc = block_loop(rd, k, block_bases, [&](const char *s, size_t l) {
+		if (seq_out && nb + l <= seq_cap) memcpy(seq_out + nb, s, l);
+		if (lens_out && nr < lens_cap) lens_out[nr] = (uint32_t)l;
+		nb += l;
+		++nr;
+		return VC_OK;
+	}, local);
+	local.seconds = wall_now() - t0;
+	*st = local;
+	return rc;
+}
+
+extern "C" int64_t vc_scan_records(const char *path, int32_t *rets, int64_t cap)
+{
+	if (!path) return VC_EINVAL;
+	VcFastqReader rd;
+	if (!rd.open(path)) return VC_EIO;
+	int64_t n = 0;
+	int ret;
+	do {
+		ret = rd.next();
+		if (n < cap && rets) rets[n] = ret;
+		++n;
+	} while (ret != -1);
+	return n;
 }
 
 // ---------------------------------------------------------------------------

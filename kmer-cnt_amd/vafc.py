@@ -36,8 +36,8 @@ EXPORTS = (
     "vc_write_vaf", "vc_pattern_fields", "vc_free", "vc_create", "vc_destroy",
     "vc_count_block", "vc_count_device", "vc_finish", "vc_reset", "vc_device_counts",
     "vc_bind_outputs", "vc_device_tally", "vc_stream", "vc_set_timing", "vc_kernel_ms",
-    "vc_table_info", "vc_count_file", "vc_synth_reads", "vc_debug_decode", "vc_strerror",
-    "vc_version",
+    "vc_table_info", "vc_count_file", "vc_scan_file", "vc_scan_records", "vc_synth_reads",
+    "vc_debug_decode", "vc_strerror", "vc_version",
 )
 
 
@@ -101,6 +101,9 @@ def lib():
         "vc_table_info": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                     C.POINTER(C.c_uint64)]),
         "vc_count_file": (C.c_int, [P, C.c_char_p, C.c_int, C.c_int, C.POINTER(FileStats)]),
+        "vc_scan_file": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(FileStats), P, C.c_size_t,
+                                   P, C.c_size_t]),
+        "vc_scan_records": (C.c_int64, [C.c_char_p, P, C.c_int64]),
         "vc_synth_reads": (C.c_int, [P, P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
                                      C.c_double, P, P, C.c_uint32, P]),
         "vc_debug_decode": (C.c_int, [P, C.c_size_t, P, P, C.c_uint64, P, P]),
@@ -291,6 +294,39 @@ def count_fastq_kmers(fn: str, k: int, n_thread: int, block_size: int, kmer_map:
         return kmer_map.count_file(fn, block_size, n_thread)
     except FileNotFoundError:
         return None
+
+
+def scan_file(fn: str, k: int, block_size: int = 10_000_000, with_reads: bool = False):
+    """Host-only reader + block loop (no device): (FileStats, reads or None)."""
+    st = FileStats()
+    if not with_reads:
+        rc = lib().vc_scan_file(fn.encode(), k, block_size, C.byref(st), None, 0, None, 0)
+        reads = None
+    else:
+        size = os.path.getsize(fn) + 16
+        seq = np.zeros(max(size * 4, 64), np.uint8)     # gz inflates; bounded by caller use
+        lens = np.zeros(max(size, 16), np.uint32)
+        rc = lib().vc_scan_file(fn.encode(), k, block_size, C.byref(st), _ptr(seq), seq.size,
+                                _ptr(lens), lens.size)
+        reads = []
+        pos = 0
+        for i in range(int(st.seqs)):
+            n = int(lens[i])
+            reads.append(seq[pos:pos + n].tobytes())
+            pos += n
+    if rc == VC_EIO:
+        raise FileNotFoundError(fn)
+    _ck(rc, "vc_scan_file")
+    return st, reads
+
+
+def scan_records(fn: str, cap: int = 1 << 20) -> np.ndarray:
+    """kseq_read return codes of every record of a file (host-only)."""
+    rets = np.zeros(cap, np.int32)
+    n = lib().vc_scan_records(fn.encode(), _ptr(rets), cap)
+    if n == VC_EIO:
+        raise FileNotFoundError(fn)
+    return rets[:min(n, cap)]
 
 
 def synth_reads(seq_ptr, offs_ptr, lens_ptr, first, n_reads, read_len, seed, f_snp,

@@ -1,0 +1,96 @@
+"""libvafc.so: loads, exports every symbol include/vafc.h declares, and its
+host-side logic (pattern loader, key table content, .vaf writer) agrees with
+the oracle -- no GPU needed."""
+import hashlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import CASES, ROOT
+
+
+def header_functions():
+    with open(os.path.join(ROOT, "include", "vafc.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vc_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    import vafc
+    L = vafc.lib()
+    declared = header_functions()
+    assert len(declared) >= 25
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    assert set(declared) == set(vafc.EXPORTS)
+    assert L.vc_version() == 1
+
+
+def test_strerror_and_nodev():
+    import ctypes as C
+    import vafc
+    L = vafc.lib()
+    assert L.vc_strerror(vafc.VC_EHIP) == b"HIP runtime error"
+    h = C.c_void_p()
+    keys = np.zeros(1, np.uint64)
+    vals = np.zeros(1, np.uint32)
+    rc = L.vc_create(C.byref(h), 40, keys.ctypes.data_as(C.c_void_p), vals.ctypes.data_as(C.c_void_p), 1, 1, 0)
+    assert rc == vafc.VC_EINVAL or rc == vafc.VC_ENODEV       # k=40 rejected (or no device)
+    import torch
+    if not torch.cuda.is_available():
+        rc = L.vc_create(C.byref(h), 21, keys.ctypes.data_as(C.c_void_p), vals.ctypes.data_as(C.c_void_p), 1, 1, 0)
+        assert rc == vafc.VC_ENODEV
+
+
+def test_missing_pattern_file():
+    import vafc
+    with pytest.raises(vafc.VafcError) as e:
+        vafc.load_patterns("/nonexistent/patterns.txt")
+    assert e.value.code == vafc.VC_EIO
+
+
+@pytest.mark.parametrize("fn,k", [("pat_k21.txt", 21), ("pat_edge_k21.txt", 21), ("pat_edge_k31.txt", 31),
+                                  ("pat_edge_k15.txt", 15), ("empty_patterns.txt", 21)])
+def test_pattern_keys_match_oracle(fn, k):
+    """create_combined_kmer_map content: same (key -> value) mapping, same collisions."""
+    import vafc
+    import oracle as O
+    db = vafc.load_patterns(os.path.join(CASES, fn))
+    keys, vals, coll = db.keys(k)
+    orc = O.Oracle(k, pattern_fn=os.path.join(CASES, fn))
+    ok, ov = orc.keys()
+    assert db.n == orc.n_patterns
+    assert coll == orc.n_collisions
+    assert dict(zip(keys.tolist(), vals.tolist())) == dict(zip(ok.tolist(), ov.tolist()))
+
+
+def test_vaf_writer_matches_reference_output(manifest, tmp_path):
+    """Host .vaf writer fed the oracle's counts reproduces the reference's file."""
+    import vafc
+    import oracle as O
+    entry = next(c for c in manifest["cases"] if c["name"] == "edge_k21")
+    orc = O.Oracle(21, pattern_fn=os.path.join(CASES, "pat_k21.txt"))
+    counts = np.zeros(2 * orc.n_patterns + 2, np.uint32)
+    rc, b, s, km = orc.count_file(os.path.join(CASES, "edge.fq"), 10_000_000, counts)
+    db = vafc.load_patterns(os.path.join(CASES, "pat_k21.txt"))
+    out = str(tmp_path / "w.vaf")
+    db.write_vaf(counts, out)
+    assert hashlib.md5(open(out, "rb").read()).hexdigest() == entry["vaf_md5"]
+
+
+def test_vaf_writer_u32_wraparound(tmp_path):
+    """TOTAL_COUNT is a uint32 sum that wraps (vaf-counter.c:673); the average is not."""
+    import vafc
+    db = vafc.load_patterns(os.path.join(CASES, "pat_k21.txt"))
+    counts = np.zeros(2 * db.n, np.uint32)
+    counts[0], counts[1] = 0xFFFFFFF0, 0x20
+    out = str(tmp_path / "wrap.vaf")
+    db.write_vaf(counts, out)
+    lines = open(out).read().splitlines()
+    f = lines[2].split("\t")
+    assert f[5:8] == [str(0xFFFFFFF0), str(0x20), str((0xFFFFFFF0 + 0x20) & 0xFFFFFFFF)]
+    assert float(f[8]) == pytest.approx(0x20 / 0x10, abs=1e-4)
+    assert lines[0] == "# Average depth: %.2f" % ((0xFFFFFFF0 + 0x20) / db.n)

@@ -1,0 +1,374 @@
+"""HIP path parity (needs an MI355X): every test calls libvafc.so through its C
+ABI and compares with the reference's goldens or the oracle, bit-exactly."""
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, PRODUCT_CLI, run_cli
+
+pytestmark = pytest.mark.gpu
+
+with open(os.path.join(GOLDEN, "manifest.json")) as _f:
+    CASE_NAMES = [c["name"] for c in json.load(_f)["cases"]]
+
+ALPHABET = np.frombuffer(b"ACGTACGTACGTACGTACGTacgtNnUuSWDQE\x00\x01\x02\x03\x80\xc1\xd4\xff -", np.uint8)
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch.device("cuda", 0)
+
+
+def random_reads(rng, lens):
+    out = []
+    for L in lens:
+        if rng.integers(0, 3) == 0:
+            out.append(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        else:
+            out.append(ALPHABET[rng.integers(0, ALPHABET.size, L)].tobytes())
+    return out
+
+
+def table_from_reads(k, reads, rng, n_pat=500):
+    """Keys drawn from k-mers that really occur (so there are hits), plus misses."""
+    import oracle as O
+    pool = np.unique(np.concatenate([O.read_kmers(k, r) for r in reads] + [np.zeros(0, np.uint64)]))
+    sel = pool[rng.permutation(pool.size)[: min(pool.size, n_pat)]] if pool.size else pool
+    mask = np.uint64((1 << (2 * k)) - 1)
+    extra = rng.integers(0, 1 << 62, 200, dtype=np.uint64) & mask
+    keys = np.concatenate([sel, extra]).astype(np.uint64)
+    vals = (np.arange(keys.size, dtype=np.uint32) % (2 * n_pat)).astype(np.uint32)
+    return keys, vals, n_pat
+
+
+def gpu_counts(k, keys, vals, n_pat, reads, blocks=1, env=None):
+    import vafc
+    import vafc_synth as S
+    old = {}
+    for kk, v in (env or {}).items():
+        old[kk] = os.environ.get(kk)
+        os.environ[kk] = v
+    try:
+        m = vafc.KmerMap(k, keys, vals, n_pat, 0)
+    finally:
+        for kk, v in old.items():
+            if v is None:
+                os.environ.pop(kk, None)
+            else:
+                os.environ[kk] = v
+    step = max(1, (len(reads) + blocks - 1) // blocks)
+    for i in range(0, len(reads), step):
+        seq, offs, lens = S.pack_reads(reads[i:i + step])
+        if seq.size == 0:
+            seq = np.zeros(1, np.uint8)
+        m.count_block(seq, offs, lens)
+    c, km = m.finish()
+    m.close()
+    return c, km
+
+
+def oracle_counts(k, keys, vals, n_pat, reads):
+    import oracle as O
+    import vafc_synth as S
+    orc = O.Oracle(k, keys=keys, vals=vals)
+    seq, offs, lens = S.pack_reads(reads)
+    if seq.size == 0:
+        seq = np.zeros(1, np.uint8)
+    return orc.count_reads(seq, offs, lens, n_patterns=n_pat)
+
+
+# --------------------------------------------------------------------------
+# the drop-in CLI on the reference's golden cases
+# --------------------------------------------------------------------------
+
+@pytest.mark.parametrize("name", CASE_NAMES)
+def test_cli_matches_reference(name, manifest, synth_dir, tmp_path):
+    entry = next(c for c in manifest["cases"] if c["name"] == name)
+    rc, stats, data, err = run_cli(PRODUCT_CLI, entry, synth_dir, tmp_path)
+    assert rc == entry["exit"], err[-2000:]
+    if entry["vaf_md5"] is not None:
+        assert hashlib.md5(data).hexdigest() == entry["vaf_md5"]
+        for key in ("bases", "seqs", "kmers"):
+            assert stats.get(key) == entry["stats"].get(key), key
+    assert ("collisions detected" in err) == entry["collision_warning"]
+
+
+@pytest.mark.parametrize("name", ["c1_plumbing_k21", "pe_k31", "edge_k15", "mal_gbbbg_b1"])
+def test_python_mirror_matches_reference(name, manifest, synth_dir, tmp_path):
+    import vafc
+    from conftest import case_dir
+    entry = next(c for c in manifest["cases"] if c["name"] == name)
+    out = str(tmp_path / "py.vaf")
+    cwd = os.getcwd()
+    os.chdir(case_dir(entry, synth_dir))
+    try:
+        rc = vafc.main(entry["argv"] + ["-o", out])
+    finally:
+        os.chdir(cwd)
+    assert rc == 0
+    assert hashlib.md5(open(out, "rb").read()).hexdigest() == entry["vaf_md5"]
+
+
+# --------------------------------------------------------------------------
+# kernels vs oracle on random inputs
+# --------------------------------------------------------------------------
+
+@pytest.mark.parametrize("k", [1, 5, 15, 16, 17, 21, 24, 31])
+def test_random_reads_vs_oracle(k):
+    rng = np.random.default_rng(k)
+    lens = list(rng.integers(0, 200, 3000)) + [0, 1, k - 1, k, k + 1, 15, 16, 17, 31, 32, 33, 150, 151, 1000, 5000]
+    reads = random_reads(rng, lens)
+    keys, vals, n_pat = table_from_reads(k, reads, rng)
+    got, km = gpu_counts(k, keys, vals, n_pat, reads, blocks=3)
+    want, km_want = oracle_counts(k, keys, vals, n_pat, reads)
+    assert km == km_want
+    assert np.array_equal(got, want)
+    assert int(want.sum()) > 0
+
+
+@pytest.mark.parametrize("k", [21, 31, 9])
+def test_long_reads_segmented_kernel(k):
+    """Reads > VC_LONG_READ (16384) take the segmented long-read kernel."""
+    rng = np.random.default_rng(77 + k)
+    lens = [16384, 16385, 20000, 65536 + 7, 300_000] + list(rng.integers(100, 300, 500))
+    reads = random_reads(rng, lens)
+    keys, vals, n_pat = table_from_reads(k, reads, rng, n_pat=2000)
+    got, km = gpu_counts(k, keys, vals, n_pat, reads)
+    want, km_want = oracle_counts(k, keys, vals, n_pat, reads)
+    assert km == km_want
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("k", [1, 5, 15, 16, 17, 21, 31])
+def test_every_kmer_of_golden_reads(k):
+    """Table = every distinct k-mer of the golden reads (whose k-mer lists are pinned
+    to the reference's extract_kmers_to_buf); GPU multiplicities must match."""
+    import oracle as O
+    z = np.load(os.path.join(GOLDEN, "kmers_k%d.npz" % k))
+    seq, lens = z["seq"], z["lens"]
+    reads, pos = [], 0
+    for L in lens:
+        reads.append(seq[pos:pos + int(L)].tobytes())
+        pos += int(L)
+    allk = np.concatenate([O.read_kmers(k, r) for r in reads])
+    uniq, mult = np.unique(allk, return_counts=True)
+    vals = np.arange(uniq.size, dtype=np.uint32)
+    n_pat = (uniq.size + 1) // 2
+    got, km = gpu_counts(k, uniq, vals, n_pat, reads)
+    assert km == allk.size == int(z["counts"].sum())
+    assert np.array_equal(got[: uniq.size], mult.astype(np.uint32))
+
+
+def test_device_decode_matches_oracle(torch_dev):
+    import torch
+    import vafc
+    import oracle as O
+    rng = np.random.default_rng(3)
+    reads = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in list(range(0, 80)) * 4 + [150, 1000]]
+    import vafc_synth as S
+    seq, offs, lens = S.pack_reads(reads)
+    d_seq = torch.from_numpy(seq).to(torch_dev)
+    d_offs = torch.from_numpy(offs.astype(np.int64)).to(torch_dev)
+    d_lens = torch.from_numpy(lens.astype(np.int32)).to(torch_dev)
+    d_codes = torch.full((seq.size,), 9, dtype=torch.uint8, device=torch_dev)
+    torch.cuda.synchronize()
+    vafc.debug_decode(d_seq.data_ptr(), seq.size, d_offs.data_ptr(), d_lens.data_ptr(), len(reads),
+                      d_codes.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = d_codes.cpu().numpy()
+    want = np.concatenate([O.decode(r) for r in reads])
+    assert np.array_equal(got, want)
+
+
+def test_device_generator_matches_numpy(torch_dev):
+    import torch
+    import vafc
+    import vafc_synth as S
+    panel = S.make_panel(S.synthetic_bed(500))
+    win = torch.from_numpy(panel.windows().reshape(-1)).to(torch_dev)
+    dos = torch.from_numpy(panel.dosage.astype(np.uint8)).to(torch_dev)
+    for first, n, L, f in ((0, 4000, 150, 0.3), (12_345_678, 3000, 150, 1.0), (5, 1000, 100, 0.0)):
+        d_seq = torch.empty(n * L, dtype=torch.uint8, device=torch_dev)
+        d_offs = torch.empty(n, dtype=torch.int64, device=torch_dev)
+        d_lens = torch.empty(n, dtype=torch.int32, device=torch_dev)
+        torch.cuda.synchronize()
+        vafc.synth_reads(d_seq.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), first, n, L, 42, f,
+                         win.data_ptr(), dos.data_ptr(), panel.n, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        want = S.gen_reads(panel, n, first=first, seed=42, f_snp=f, read_len=L)
+        assert np.array_equal(d_seq.cpu().numpy().reshape(n, L), want)
+        assert np.array_equal(d_offs.cpu().numpy(), np.arange(n) * L)
+        assert np.all(d_lens.cpu().numpy() == L)
+
+
+def test_device_resident_unaligned_and_filters(torch_dev):
+    """count_device on HBM reads at every byte misalignment, both LDS filter layouts."""
+    import torch
+    import vafc
+    import vafc_synth as S
+    import oracle as O
+    import tempfile
+    panel = S.make_panel(S.synthetic_bed(3000))
+    with tempfile.TemporaryDirectory() as d:
+        pat = os.path.join(d, "p.txt")
+        panel.write_patterns(pat, 21)
+        db = vafc.load_patterns(pat)
+        keys, vals, _ = db.keys(21)
+        reads = S.gen_reads(panel, 20000, f_snp=0.5)
+        seq, offs, lens = S.pack_reads(reads)
+        want, km_want = O.Oracle(21, pattern_fn=pat).count_reads(seq, offs, lens)
+    res = []
+    for fw in ("64", "32"):
+        os.environ["VAFC_FILTER"] = fw
+        try:
+            m = vafc.KmerMap(21, keys, vals, db.n, 0)
+        finally:
+            os.environ.pop("VAFC_FILTER", None)
+        for mis in range(4):
+            buf = torch.zeros(seq.size + 8, dtype=torch.uint8, device=torch_dev)
+            buf[mis:mis + seq.size] = torch.from_numpy(seq).to(torch_dev)
+            d_offs = torch.from_numpy(offs.astype(np.int64)).to(torch_dev)
+            d_lens = torch.from_numpy(lens.astype(np.int32)).to(torch_dev)
+            torch.cuda.synchronize()
+            m.reset()
+            m.count_device(buf.data_ptr() + mis, seq.size, d_offs.data_ptr(), d_lens.data_ptr(), lens.size)
+            got, km = m.finish()
+            assert km == km_want, (fw, mis)
+            assert np.array_equal(got, want), (fw, mis)
+            res.append(int(got.sum()))
+        m.close()
+    assert min(res) > 0
+
+
+def test_count_file_equals_oracle_file_pass(tmp_path):
+    """The product's streaming file path (pinned batches, -b blocks) on a 300k-read FASTQ."""
+    import vafc
+    import vafc_synth as S
+    import oracle as O
+    panel = S.grch38_panel()
+    pat = str(tmp_path / "p.txt")
+    panel.write_patterns(pat, 21)
+    fq = str(tmp_path / "r.fq")
+    S.write_fastq(fq, panel, 300_000, seed=7, f_snp=0.2)
+    db = vafc.load_patterns(pat)
+    m = vafc.create_combined_kmer_map(db, 21)
+    st = m.count_file(fq, 10_000_000, 4)
+    got, km = m.finish()
+    orc = O.Oracle(21, pattern_fn=pat)
+    want = np.zeros(2 * orc.n_patterns + 2, np.uint32)
+    rc, bases, seqs, km_want = orc.count_file(fq, 10_000_000, want)
+    assert (st.bases, st.seqs) == (bases, seqs)
+    assert km == km_want
+    assert np.array_equal(got, want[: 2 * orc.n_patterns])
+
+
+def test_large_panel_c5_shape():
+    """C5 shape: a 200k-SNP panel (~400k keys, saturated LDS prefilter)."""
+    import vafc
+    import vafc_synth as S
+    import oracle as O
+    import tempfile
+    panel = S.make_panel(S.synthetic_bed(200_000))
+    with tempfile.TemporaryDirectory() as d:
+        pat = os.path.join(d, "p.txt")
+        panel.write_patterns(pat, 21)
+        db = vafc.load_patterns(pat)
+        keys, vals, coll = db.keys(21)
+        reads = S.gen_reads(panel, 60_000, f_snp=0.5)
+        seq, offs, lens = S.pack_reads(reads)
+        want, km_want = O.Oracle(21, pattern_fn=pat).count_reads(seq, offs, lens)
+    m = vafc.KmerMap(21, keys, vals, db.n, 0)
+    m.count_block(seq, offs, lens)
+    got, km = m.finish()
+    assert km == km_want and np.array_equal(got, want)
+    assert int(got.sum()) > 20_000
+
+
+def test_full_size_linearity_and_prefix_parity(torch_dev):
+    """At BASELINE size (100M reads, HBM-resident): count(all) == count(first half) +
+    count(second half) (mod 2^32), k-mer tallies add up, and an exact 1M-read prefix
+    matches the oracle."""
+    import torch
+    import vafc
+    import vafc_synth as S
+    import oracle as O
+    import tempfile
+    panel = S.grch38_panel()
+    R, L = 100_000_000, 150
+    d_seq = torch.empty(R * L, dtype=torch.uint8, device=torch_dev)
+    d_offs = torch.empty(R, dtype=torch.int64, device=torch_dev)
+    d_lens = torch.empty(R, dtype=torch.int32, device=torch_dev)
+    win = torch.from_numpy(panel.windows().reshape(-1)).to(torch_dev)
+    dos = torch.from_numpy(panel.dosage.astype(np.uint8)).to(torch_dev)
+    torch.cuda.synchronize()
+    vafc.synth_reads(d_seq.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), 0, R, L, 42, 0.01,
+                     win.data_ptr(), dos.data_ptr(), panel.n, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    with tempfile.TemporaryDirectory() as d:
+        pat = os.path.join(d, "p.txt")
+        panel.write_patterns(pat, 21)
+        db = vafc.load_patterns(pat)
+        keys, vals, _ = db.keys(21)
+        orc = O.Oracle(21, pattern_fn=pat)
+    m = vafc.KmerMap(21, keys, vals, db.n, 0)
+
+    def run(first, n):
+        m.reset()
+        m.count_device(d_seq.data_ptr() + first * L, n * L, d_offs.data_ptr(), d_lens.data_ptr(), n)
+        return m.finish()
+
+    all_c, all_k = run(0, R)
+    h = R // 2
+    a_c, a_k = run(0, h)
+    # second half: offsets are absolute, so pass the offsets tail with the full base
+    m.reset()
+    m.count_device(d_seq.data_ptr(), R * L, d_offs.data_ptr() + h * 8, d_lens.data_ptr() + h * 4, R - h)
+    b_c, b_k = m.finish()
+    assert all_k == a_k + b_k
+    assert np.array_equal(all_c, (a_c.astype(np.uint64) + b_c).astype(np.uint32))
+    assert all_k > R * 120
+    n = 1_000_000
+    p_c, p_k = run(0, n)
+    seq = d_seq[: n * L].cpu().numpy()
+    want, km_want = orc.count_reads(seq, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint32))
+    assert p_k == km_want and np.array_equal(p_c, want)
+    m.close()
+
+
+def test_bound_outputs_accumulate_and_wrap(torch_dev):
+    """Counts bound to a caller buffer accumulate modulo 2^32 (uint32 semantics)."""
+    import torch
+    import vafc
+    import vafc_synth as S
+    rng = np.random.default_rng(5)
+    reads = random_reads(rng, [150] * 2000)
+    keys, vals, n_pat = table_from_reads(21, reads, rng, n_pat=100)
+    want, km_want = oracle_counts(21, keys, vals, n_pat, reads)
+    m = vafc.KmerMap(21, keys, vals, n_pat, 0)
+    start = np.full(2 * n_pat, 0xFFFFFFF0, np.uint32)
+    t = torch.from_numpy(start.view(np.int32).copy()).to(torch_dev)
+    tally = torch.zeros(1, dtype=torch.int64, device=torch_dev)
+    m.bind_outputs(t.data_ptr(), tally.data_ptr())
+    seq, offs, lens = S.pack_reads(reads)
+    m.count_block(seq, offs, lens)
+    m.finish()
+    got = t.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, ((start.astype(np.uint64) + want) & 0xFFFFFFFF).astype(np.uint32))
+    assert int(tally.item()) == km_want
+    m.close()
+
+
+def test_empty_inputs():
+    import vafc
+    m = vafc.KmerMap(21, np.zeros(0, np.uint64), np.zeros(0, np.uint32), 3, 0)
+    m.count_block(np.zeros(1, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32))
+    m.count_block(np.frombuffer(b"ACGTN" * 10, np.uint8), np.array([0, 10], np.uint64), np.array([5, 20], np.uint32))
+    c, km = m.finish()
+    assert int(c.sum()) == 0 and km == 0
+    m.close()

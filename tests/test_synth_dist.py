@@ -1,0 +1,117 @@
+"""Synthetic workload generator, rank sharding and the count all-reduce (gloo,
+world_size 2, CPU), and the Python CLI mirror's option parsing."""
+import os
+
+import numpy as np
+import pytest
+
+
+def test_generator_is_counter_based():
+    import vafc_synth as S
+    p = S.make_panel(S.synthetic_bed(50))
+    a = S.gen_reads(p, 100, first=0, f_snp=0.3)
+    b = S.gen_reads(p, 60, first=40, f_snp=0.3)
+    assert np.array_equal(a[40:], b)                     # any slice regenerates alone
+    assert set(np.unique(a).tolist()) <= set(b"ACGTN")
+    rc = (S.h64(S.READ_SEED_R1, np.arange(100, dtype=np.uint64), 3) & np.uint64(1)) == 1
+    assert 20 < int(rc.sum()) < 80
+
+
+def test_panel_kmers_place_snp_like_snp_pattern_gen():
+    import vafc_synth as S
+    p = S.make_panel(S.synthetic_bed(10))
+    for k in (21, 31, 20):
+        ref, alt = p.kmers(k)
+        assert ref.shape == (10, k)
+        assert np.array_equal(ref[:, k // 2], p.ref) and np.array_equal(alt[:, k // 2], p.alt)
+        diff = (ref != alt).sum(axis=1)
+        assert np.all(diff == 1)
+
+
+def test_snp_reads_hit_patterns():
+    """Reads cut from SNP windows contain their pattern k-mer (counts are non-trivial)."""
+    import vafc_synth as S
+    import oracle as O
+    import tempfile
+    p = S.make_panel(S.synthetic_bed(200))
+    with tempfile.TemporaryDirectory() as d:
+        pat = os.path.join(d, "p.txt")
+        p.write_patterns(pat, 21)
+        orc = O.Oracle(21, pattern_fn=pat)
+        seq, offs, lens = S.pack_reads(S.gen_reads(p, 2000, f_snp=1.0))
+        counts, km = orc.count_reads(seq, offs, lens)
+    assert km > 2000 * 120
+    assert 1200 < int(counts.sum()) < 2000
+
+
+@pytest.mark.parametrize("n,world", [(10, 3), (100, 8), (7, 8), (0, 2)])
+def test_shard_partition(n, world):
+    from vafc_dist import shard
+    parts = [shard(n, r, world) for r in range(world)]
+    assert sum(c for _, c in parts) == n
+    pos = 0
+    for first, c in parts:
+        assert first == pos
+        pos += c
+    assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+
+
+def _rank_main(rank, world, port, pat, reads_path, out_path):
+    import torch.distributed as dist
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "kmer-cnt_amd"))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "oracle"))
+    import oracle as O
+    import vafc_dist as D
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    z = np.load(reads_path)
+    seq, offs, lens = z["seq"], z["offs"], z["lens"]
+    first, cnt = D.shard(lens.size, rank, world)
+    orc = O.Oracle(21, pattern_fn=pat)       # CPU stand-in for the per-GPU counter
+    counts, km = orc.count_reads(seq, offs[first:first + cnt], lens[first:first + cnt])
+    if rank == 0:
+        counts[0] = np.uint32((int(counts[0]) + 0xFFFFFFFF) & 0xFFFFFFFF)   # force a wrap
+    t = D.counts_to_tensor(counts)
+    D.allreduce_counts(t)
+    total_km = D.allreduce_u64(int(km))
+    if rank == 0:
+        np.savez(out_path, counts=D.tensor_to_counts(t), kmers=np.array([total_km], np.uint64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_allreduce_of_sharded_counts_is_bit_exact(tmp_path):
+    import socket
+    import torch.multiprocessing as mp
+    import vafc_synth as S
+    import oracle as O
+    p = S.make_panel(S.synthetic_bed(300))
+    pat = str(tmp_path / "p.txt")
+    p.write_patterns(pat, 21)
+    seq, offs, lens = S.pack_reads(S.gen_reads(p, 3001, f_snp=0.7))
+    rp = str(tmp_path / "reads.npz")
+    np.savez(rp, seq=seq, offs=offs, lens=lens)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "out.npz")
+    mp.start_processes(_rank_main, args=(2, port, pat, rp, out), nprocs=2, join=True, start_method="spawn")
+    got = np.load(out)
+    orc = O.Oracle(21, pattern_fn=pat)
+    want, km = orc.count_reads(seq, offs, lens)
+    want = want.copy()
+    want[0] = np.uint32((int(want[0]) + 0xFFFFFFFF) & 0xFFFFFFFF)   # same forced wrap
+    assert np.array_equal(got["counts"], want)
+    assert int(got["kmers"][0]) == km
+
+
+def test_cli_option_parsing_mirror():
+    import vafc
+    o, files = vafc.parse_args(["a.fq", "-k", "31", "-p", "pat.txt", "b.fq", "-vt8", "-o", "x.vaf", "-b1"])
+    assert files == ["a.fq", "b.fq"]
+    assert (o["k"], o["p"], o["o"], o["t"], o["b"], o["v"]) == (31, "pat.txt", "x.vaf", 8, 1, True)
+    o, files = vafc.parse_args(["-p", "p", "-o", "o", "--", "-weird.fq"])
+    assert files == ["-weird.fq"]
+    assert vafc.main(["-p", "p.txt"]) == 1                      # usage -> exit 1
