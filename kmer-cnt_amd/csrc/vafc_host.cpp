@@ -231,6 +231,7 @@ struct vc_ctx {
 	int n_cu = 256;
 	vc_slot_t *d_table = nullptr;
 	int filter_w = VC_FILTER_W64;
+	int ablate = 0;                   // kernel ablation variant (libvafc_abl.so only)
 	uint32_t tbits = 0;
 	uint32_t *d_filter = nullptr;
 	uint32_t wbits = 0;
@@ -285,10 +286,10 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	while (((uint64_t)1 << tbits) < 2 * (uint64_t)n_keys + 2) ++tbits;
 	const uint64_t tslots = (uint64_t)1 << tbits;
 	std::vector<vc_slot_t> tab(tslots, vc_slot_t{VC_EMPTY_KEY, 0u, 0u});
-	// LDS prefilter: >= 24 bits per key, 1 KiB .. 128 KiB; 64-bit words with
-	// 4 bits per key (default) or 32-bit words with 2 bits (VAFC_FILTER=32)
+	// LDS prefilter: >= 24 bits per key, 1 KiB .. 128 KiB; 32-bit words with
+	// 2 bits per key (default) or 64-bit words with 4 bits (VAFC_FILTER=64)
 	const char *fenv = getenv("VAFC_FILTER");
-	const int filter_w = (fenv && atoi(fenv) == 32) ? VC_FILTER_W32 : VC_FILTER_W64;
+	const int filter_w = (fenv && atoi(fenv) == 64) ? VC_FILTER_W64 : VC_FILTER_W32;
 	uint32_t wbits = 8;
 	while (wbits < VC_MAX_FILTER_WBITS && ((uint64_t)32 << wbits) < 24 * (uint64_t)n_keys) ++wbits;
 	std::vector<uint32_t> fw((size_t)1 << wbits, 0);
@@ -320,6 +321,7 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	c->tbits = tbits;
 	c->wbits = wbits;
 	c->filter_w = filter_w;
+	c->ablate = getenv("VAFC_ABLATE") ? atoi(getenv("VAFC_ABLATE")) : 0;
 
 	int rc = VC_OK;
 #define TRY(call)                                                                        \
@@ -415,6 +417,7 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 	A.filter = c->d_filter;
 	A.wbits = c->wbits;
 	A.filter_w = c->filter_w;
+	A.ablate = c->ablate;
 	A.k = c->k;
 	A.kmask = ((uint64_t)1 << (2 * c->k)) - 1;
 	A.counts = c->d_counts;

@@ -11,7 +11,7 @@
 #include "vafc_common.h"
 
 #define VC_BLOCK 1024        // threads per block: 16 waves, one block per CU
-#define VC_QCAP 128          // per-wave LDS queue entries
+#define VC_QCAP 240          // per-wave LDS queue entries (u64): 16 waves x 1920 B + 128 KiB filter fit in 160 KiB
 
 struct VcKernelArgs {
 	const uint8_t *seq;          // 4-byte aligned base of the read bytes
@@ -25,6 +25,7 @@ struct VcKernelArgs {
 	const uint32_t *filter;      // 2^wbits 32-bit words (2^(wbits-1) 64-bit words)
 	uint32_t wbits;
 	int filter_w;                // VC_FILTER_W32 or VC_FILTER_W64
+	int ablate;                  // ablation builds only (VAFC_ABLATE), 0 otherwise
 	int k;
 	uint64_t kmask;              // (1 << 2k) - 1
 	uint32_t *counts;            // [2 * n_patterns]

@@ -156,8 +156,50 @@ struct WaveQueue {
 	uint32_t n;      // wave-uniform fill
 };
 
-// Lanes with `hit` append `key` (bal = ballot(hit) != 0); a queue holding a
-// full wave's worth is drained by all 64 lanes probing the table at once.
+// Probe the exact table for queue entries [lo, hi) (up to 4 per lane); the
+// first table load of every entry is issued before any is resolved, so one
+// memory latency covers the whole drain.
+__device__ __forceinline__ void drain_range(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
+                                            uint32_t hi, int lane)
+{
+	__builtin_amdgcn_wave_barrier();
+	uint64_t key[4];
+	uint32_t s[4];
+	uint4 e[4];
+#pragma unroll
+	for (int r = 0; r < 4; ++r) {
+		const uint32_t i = lo + (uint32_t)(r * WAVE + lane);
+		key[r] = VC_EMPTY_KEY;
+		s[r] = 0;
+		if (i < hi) {
+			const uint64_t f = q[i] & A.kmask;
+			const uint64_t rc = revcomp_dev(f, A.k);
+			key[r] = f < rc ? f : rc;
+			s[r] = vc_table_slot(vc_hash(key[r]), A.tbits);
+			e[r] = *reinterpret_cast<const uint4 *>(&A.table[s[r]]);
+		}
+	}
+#pragma unroll
+	for (int r = 0; r < 4; ++r) {
+		if (key[r] == VC_EMPTY_KEY) continue;
+		uint4 x = e[r];
+		uint32_t t = s[r];
+		for (;;) {
+			const uint64_t k2 = ((uint64_t)x.y << 32) | x.x;
+			if (k2 == key[r]) {
+				atomicAdd(&A.counts[x.z], 1u);
+				break;
+			}
+			if (k2 == VC_EMPTY_KEY) break;
+			t = (t + 1u) & A.tmask;
+			x = *reinterpret_cast<const uint4 *>(&A.table[t]);
+		}
+	}
+}
+
+// Lanes with `hit` append `key` (bal = ballot(hit) != 0).  The queue is
+// normally drained once per read group (queue_flush); only a nearly full
+// queue is drained here, 64 entries from its top.
 __device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q, uint64_t bal,
                                              bool hit, uint64_t key, int lane)
 {
@@ -165,22 +207,15 @@ __device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q
 	                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
 	if (hit) Q.q[Q.n + pre] = key;
 	Q.n = __builtin_amdgcn_readfirstlane(Q.n + (uint32_t)__popcll(bal));
-	if (Q.n >= WAVE) {
-		__builtin_amdgcn_wave_barrier();
-		const uint64_t k0 = Q.q[lane];
-		const uint32_t rest = Q.n - WAVE;
-		const uint64_t k1 = Q.q[lane + WAVE];
-		__builtin_amdgcn_wave_barrier();
-		if ((uint32_t)lane < rest) Q.q[lane] = k1;
-		Q.n = rest;
-		probe_and_count(A, k0);
+	if (Q.n > VC_QCAP - WAVE) {
+		drain_range(A, Q.q, Q.n - WAVE, Q.n, lane);
+		Q.n -= WAVE;
 	}
 }
 
 __device__ __forceinline__ void queue_flush(const VcKernelArgs &A, WaveQueue &Q, int lane)
 {
-	__builtin_amdgcn_wave_barrier();
-	if ((uint32_t)lane < Q.n) probe_and_count(A, Q.q[lane]);
+	if (Q.n) drain_range(A, Q.q, 0, Q.n, lane);
 	Q.n = 0;
 }
 
@@ -252,11 +287,14 @@ __device__ __forceinline__ uint64_t canonical_of(uint32_t flo, uint32_t fhi, uin
 // valid position range [vlo, vhi) (vlo = 0, vhi = len for a whole read).
 // Returns nothing; the wave's count of valid k-mers accumulates in `tally`
 // (wave-uniform).
-template <int K, bool W64, bool HAS_LO>
+// ABL (ablation builds only, -DVC_ABLATION; results are wrong by design):
+//   1 = no LDS filter reads, 2 = no global read-byte loads, 4 = no queue appends,
+//   8 = no filter stage at all (rolling + validity only)
+template <int K, bool W64, bool HAS_LO, int ABL = 0>
 __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
                                           uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
                                           int vlo, int vhi, int nit, const uint32_t *__restrict__ filt,
-                                          WaveQueue &Q, uint32_t &tally, int lane)
+                                          WaveQueue &Q, unsigned long long &tally, int lane)
 {
 	const uint32_t wbits = A.wbits;
 	const uint32_t zero_word = 1u << wbits;     // an all-zero LDS word past the filter
@@ -266,18 +304,26 @@ __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t 
 	uint64_t wi = addr >> 2;
 	const uint32_t sh = (uint32_t)(addr & 3u);
 	uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
+	uint32_t x1 = 0, x2 = 0, x3 = 0, x4 = 0;
 	if (c_lo < c_hi) {
 		ld4(s32, wi, wmax, w0, w1, w2, w3);
 		w4 = ldw(s32, wi + 4, wmax);
 	}
+	if (c_lo + 1 < c_hi) ld4(s32, wi + 5, wmax, x1, x2, x3, x4);
 	Roller<K> R;
 	R.init(A);
 
 	for (int it = 0; it < nit; ++it) {
 		const int c = c_lo + it;
-		// next chunk's dwords are in flight while this chunk is processed
-		uint32_t x1 = 0, x2 = 0, x3 = 0, x4 = 0;
-		if (c + 1 < c_hi) ld4(s32, wi + 5, wmax, x1, x2, x3, x4);
+		// the dwords of the next two chunks are in flight while this one is processed
+		uint32_t y1 = 0, y2 = 0, y3 = 0, y4 = 0;
+		if (c + 2 < c_hi) {
+			if constexpr ((ABL & 2) != 0) {
+				y1 = (uint32_t)wi * 0x9E3779B1u; y2 = y1 ^ 0x41434754u; y3 = y1 + 0x54474341u; y4 = y1 * 5u;
+			} else {
+				ld4(s32, wi + 9, wmax, y1, y2, y3, y4);
+			}
+		}
 		const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
 		const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
 		const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
@@ -312,17 +358,20 @@ __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t 
 				const uint32_t x = tw >> (8 * (j & 3));
 				R.push(x & 3u, x >> 2);
 				const bool valid = R.valid();
-				tally += valid ? 1u : 0u;
+				tally += (unsigned long long)__popcll(__ballot(valid));
 				const uint32_t fx = R.fx();
 				if constexpr (W64) {
 					const uint32_t widx = valid ? vc_filter_word(fx, wbits - 1u) : (zero_word >> 1);
-					const uint2 w = reinterpret_cast<const uint2 *>(filt)[widx];
+					uint2 w;
+					if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); w = make_uint2(widx, widx); }
+					else w = reinterpret_cast<const uint2 *>(filt)[widx];
 					fw[j] = w.x;
 					fw2[j] = w.y;
 					fys[j] = R.flo ^ R.rlo;
 				} else {
 					const uint32_t widx = valid ? vc_filter_word(fx, wbits) : zero_word;
-					fw[j] = filt[widx];
+					if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); fw[j] = 0u; }
+					else fw[j] = filt[widx];
 				}
 				fxs[j] = fx;
 				fl[j] = R.flo; fh[j] = R.fhi;
@@ -338,12 +387,203 @@ __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t 
 					hit = (fw[j] & fm) == fm;
 				}
 				const uint64_t bal = __ballot(hit);
-				if (bal) queue_append(A, Q, bal, hit, ((uint64_t)fh[j] << 32) | fl[j], lane);
+				if constexpr ((ABL & 4) != 0) { asm volatile("" :: "s"(bal)); }
+				else if (bal) queue_append(A, Q, bal, hit, ((uint64_t)fh[j] << 32) | fl[j], lane);
 			}
 		}
 		w0 = w4; w1 = x1; w2 = x2; w3 = x3; w4 = x4;
+		x1 = y1; x2 = y2; x3 = y3; x4 = y4;
 		wi += 4;
 	}
+}
+
+// ---------------------------------------------------------------------------
+// packed-stream scan for compile-time k in 17..31 (the hot path)
+// ---------------------------------------------------------------------------
+//
+// Each 16-base chunk is packed once into 2-bit streams:
+//   L  little-endian codes, base j at bits 2j           (complemented: C = ~L)
+//   B  big-endian codes,    base j at bits 2(15-j)      (pair-reversed L)
+// The forward k-mer's low 32 bits at base j are one v_alignbit of (B[c-1]:B[c])
+// and the reverse complement's low 32 bits one v_alignbit of the C stream, with
+// compile-time shifts; the prefilter hash fx = lo32(fwd) + lo32(rc) needs
+// nothing else.  Hits set bits of a per-lane 16-bit mask; only at the end of a
+// chunk, and only if some lane of the wave has a hit, are the full forward
+// k-mers of the hit positions extracted (variable shift) and queued.
+
+// 4x4 transpose of 2-bit fields: (byte r, field c) <-> (byte c, field r).
+__device__ __forceinline__ uint32_t transpose2x4x4(uint32_t a)
+{
+	uint32_t t = ((a >> 6) ^ a) & 0x00CC00CCu;
+	a ^= t ^ (t << 6);
+	t = ((a >> 12) ^ a) & 0x0000F0F0u;
+	a ^= t ^ (t << 12);
+	return a;
+}
+
+// Reverse the order of the 16 2-bit fields of a word.
+__device__ __forceinline__ uint32_t pairrev(uint32_t x)
+{
+	x = __builtin_bitreverse32(x);
+	return ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
+}
+
+template <int K, bool W64, bool HAS_LO, int ABL = 0>
+__device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
+                                                 uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
+                                                 int vlo, int vhi, int nit,
+                                                 const uint32_t *__restrict__ filt, WaveQueue &Q,
+                                                 unsigned long long &tally, int lane)
+{
+	static_assert(K >= 17 && K <= 31, "packed scan needs 17 <= k <= 31");
+	constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
+	constexpr uint32_t VTHR = 1u << (32 - K);
+	const uint32_t wbits = A.wbits;
+	const int tail_c = (len & 15) ? (len >> 4) : -1;
+
+	uint64_t addr = off + 16ull * (uint64_t)c_lo;
+	uint64_t wi = addr >> 2;
+	const uint32_t sh = (uint32_t)(addr & 3u);
+	uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
+	uint32_t x1 = 0, x2 = 0, x3 = 0, x4 = 0;
+	if (c_lo < c_hi) {
+		ld4(s32, wi, wmax, w0, w1, w2, w3);
+		w4 = ldw(s32, wi + 4, wmax);
+	}
+	if (c_lo + 1 < c_hi) ld4(s32, wi + 5, wmax, x1, x2, x3, x4);
+
+	uint32_t Bm1 = 0, Bm2 = 0, Cm1 = 0, Cm2 = 0;   // streams of the two previous chunks
+	uint32_t inv = 0xFFFFFFFFu;                     // invalid flags, newest in bit 31
+
+	for (int it = 0; it < nit; ++it) {
+		const int c = c_lo + it;
+		uint32_t y1 = 0, y2 = 0, y3 = 0, y4 = 0;
+		if (c + 2 < c_hi) {
+			if constexpr ((ABL & 2) != 0) {
+				y1 = (uint32_t)wi * 0x9E3779B1u; y2 = y1 ^ 0x41434754u; y3 = y1 + 0x54474341u; y4 = y1 * 5u;
+			} else {
+				ld4(s32, wi + 9, wmax, y1, y2, y3, y4);
+			}
+		}
+		const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+		const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+		const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+		const uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
+		uint32_t t0 = dec_head(b0), t1 = dec_head(b1), t2 = dec_head(b2), t3 = dec_head(b3);
+		if (__ballot(c == tail_c)) {
+			if (c == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
+		}
+		const int P = 16 * c;
+		if (__ballot(P + 16 > vhi)) {
+			t0 |= range_mask_hi(vhi - P);
+			t1 |= range_mask_hi(vhi - P - 4);
+			t2 |= range_mask_hi(vhi - P - 8);
+			t3 |= range_mask_hi(vhi - P - 12);
+		}
+		if (HAS_LO) {
+			if (__ballot(P < vlo)) {
+				t0 |= range_mask_lo(vlo - P);
+				t1 |= range_mask_lo(vlo - P - 4);
+				t2 |= range_mask_lo(vlo - P - 8);
+				t3 |= range_mask_lo(vlo - P - 12);
+			}
+		}
+		// pack the chunk's codes: byte r of A holds bases r, 4+r, 8+r, 12+r
+		const uint32_t Am = (t0 & 0x03030303u) | ((t1 & 0x03030303u) << 2) |
+		                    ((t2 & 0x03030303u) << 4) | ((t3 & 0x03030303u) << 6);
+		const uint32_t L = transpose2x4x4(Am);          // base j at bits 2j
+		const uint32_t Cc = ~L;                          // complement codes, little-endian
+		const uint32_t Bc = pairrev(L);                  // big-endian codes
+
+		uint32_t hm = 0;                                 // hit bit (15 - j) for base j
+#pragma unroll
+		for (int half = 0; half < 2; ++half) {
+			const uint32_t ta = half ? t2 : t0, tb = half ? t3 : t1;
+			uint32_t fw[8], fxs[8], fw2[8], fys[8];
+			uint64_t vld[8];                             // valid windows, one wave mask per base
+#pragma unroll
+			for (int jj = 0; jj < 8; ++jj) {
+				const int j = half * 8 + jj;
+				const uint32_t tw = jj < 4 ? ta : tb;
+				inv = __builtin_amdgcn_alignbit(tw >> (8 * (j & 3) + 2), inv, 1);
+				vld[jj] = __ballot(inv < VTHR);
+				tally += (unsigned long long)__popcll(vld[jj]);   // wave-uniform, SALU
+				const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, (uint32_t)(2 * (15 - j)));
+				const int s2 = j - K + 1 + 32;             // window start relative to chunk c-2
+				uint32_t rlo;
+				if (s2 >= 16) rlo = __builtin_amdgcn_alignbit(Cc, Cm1, (uint32_t)(2 * (s2 - 16)));
+				else rlo = __builtin_amdgcn_alignbit(Cm1, Cm2, (uint32_t)(2 * s2));
+				const uint32_t fx = flo + rlo;
+				// invalid windows read some filter word; their hits are masked below
+				if constexpr (W64) {
+					const uint32_t widx = vc_filter_word(fx, wbits - 1u);
+					uint2 w;
+					if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); w = make_uint2(widx, widx); }
+					else w = reinterpret_cast<const uint2 *>(filt)[widx];
+					fw[jj] = w.x;
+					fw2[jj] = w.y;
+					fys[jj] = flo ^ rlo;
+				} else {
+					const uint32_t widx = vc_filter_word(fx, wbits);
+					if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); fw[jj] = 0u; }
+					else fw[jj] = filt[widx];
+				}
+				fxs[jj] = fx;
+			}
+#pragma unroll
+			for (int jj = 0; jj < 8; ++jj) {
+				bool pass;
+				if constexpr (W64) {
+					const uint32_t ml = vc_filter_mask_lo(fxs[jj]), mh = vc_filter_mask_hi(fxs[jj], fys[jj]);
+					pass = (((fw[jj] & ml) ^ ml) | ((fw2[jj] & mh) ^ mh)) == 0u;
+				} else {
+					const uint32_t fm = vc_filter_mask(fxs[jj]);
+					pass = (fw[jj] & fm) == fm;
+				}
+				// hm = 2*hm + hit with the hit wave mask as carry-in: one v_addc
+				const uint64_t hb = __ballot(pass) & vld[jj];
+				uint64_t cout;
+				asm volatile("v_addc_co_u32 %0, %1, %2, %2, %3" : "=v"(hm), "=s"(cout) : "v"(hm), "s"(hb));
+				(void)cout;
+			}
+		}
+		// queue the hit positions' forward k-mers (bit b <-> base j = 15 - b)
+		if constexpr ((ABL & 4) != 0) {
+			asm volatile("" :: "v"(hm));
+		} else if (__ballot(hm != 0u)) {
+			for (;;) {
+				const bool has = hm != 0u;
+				const uint64_t bal = __ballot(has);
+				if (!bal) break;
+				const uint32_t b = has ? 31u - (uint32_t)__builtin_clz(hm) : 0u;
+				const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, 2u * b);
+				const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
+				queue_append(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
+				hm &= ~(1u << b);
+			}
+		}
+		Bm2 = Bm1; Bm1 = Bc;
+		Cm2 = Cm1; Cm1 = Cc;
+		w0 = w4; w1 = x1; w2 = x2; w3 = x3; w4 = x4;
+		x1 = y1; x2 = y2; x3 = y3; x4 = y4;
+		wi += 4;
+	}
+}
+
+// k in 17..31 with a compile-time specialisation: packed streams; otherwise
+// the general rolling scan.
+template <int K, bool W64, bool HAS_LO, int ABL = 0>
+__device__ __forceinline__ void scan_any(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
+                                         uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
+                                         int vlo, int vhi, int nit, const uint32_t *__restrict__ filt,
+                                         WaveQueue &Q, unsigned long long &tally, int lane)
+{
+	if constexpr (K >= 17)
+		scan_span_packed<K, W64, HAS_LO, ABL>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q,
+		                                       tally, lane);
+	else
+		scan_span<K, W64, HAS_LO, ABL>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tally,
+		                               lane);
 }
 
 __device__ __forceinline__ void load_filter(const VcKernelArgs &A, uint32_t *filt)
@@ -360,7 +600,7 @@ __device__ __forceinline__ void load_filter(const VcKernelArgs &A, uint32_t *fil
 // kernel 1: whole reads, one lane per read
 // ---------------------------------------------------------------------------
 
-template <int K, bool W64>
+template <int K, bool W64, int ABL = 0>
 __global__ void __launch_bounds__(VC_BLOCK)
 vc_count_reads_kernel(VcKernelArgs A)
 {
@@ -375,7 +615,7 @@ vc_count_reads_kernel(VcKernelArgs A)
 
 	const uint32_t *s32 = reinterpret_cast<const uint32_t *>(A.seq);
 	const uint64_t wmax = A.seq_words ? A.seq_words - 1 : 0;
-	uint32_t tally = 0;
+	unsigned long long tally = 0;
 
 	for (uint64_t g = blockIdx.x; g * (uint64_t)VC_BLOCK < A.n_reads; g += gridDim.x) {
 		const uint64_t r = g * (uint64_t)VC_BLOCK + threadIdx.x;
@@ -392,10 +632,11 @@ vc_count_reads_kernel(VcKernelArgs A)
 		}
 		const int nch = (len + 15) >> 4;
 		const int nit = wave_max_i32(nch);
-		scan_span<K, W64, false>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tally, lane);
+		scan_any<K, W64, false, ABL>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tally, lane);
+		queue_flush(A, Q, lane);     // one drain per read group, probes overlapped
 	}
 	queue_flush(A, Q, lane);
-	const unsigned long long t = wave_sum_u64(tally);
+	const unsigned long long t = tally;      // wave-uniform count
 	if (lane == 0 && t) atomicAdd(A.tally, t);
 }
 
@@ -422,7 +663,7 @@ vc_count_long_kernel(VcKernelArgs A)
 	const uint32_t *s32 = reinterpret_cast<const uint32_t *>(A.seq);
 	const uint64_t wmax = A.seq_words ? A.seq_words - 1 : 0;
 	const int k = K ? K : A.k;
-	uint32_t tally = 0;
+	unsigned long long tally = 0;
 	const uint64_t stride = (uint64_t)gridDim.x * VC_BLOCK;
 
 	for (uint32_t li = 0; li < nl; ++li) {
@@ -442,11 +683,11 @@ vc_count_long_kernel(VcKernelArgs A)
 				c_hi = (vhi + 15) >> 4;
 			}
 			const int nit = wave_max_i32(c_hi - c_lo);
-			scan_span<K, W64, true>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tally, lane);
+			scan_any<K, W64, true>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tally, lane);
 		}
 	}
 	queue_flush(A, Q, lane);
-	const unsigned long long t = wave_sum_u64(tally);
+	const unsigned long long t = tally;      // wave-uniform count
 	if (lane == 0 && t) atomicAdd(A.tally, t);
 }
 
@@ -542,20 +783,34 @@ __global__ void vc_synth_kernel(uint8_t *seq, uint64_t *offs, uint32_t *lens, ui
 // launchers
 // ---------------------------------------------------------------------------
 
-template <int K, bool W64>
+template <int K, bool W64, int ABL = 0>
 static hipError_t launch_kw(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
 {
 	const size_t lds = vc_lds_bytes(A->wbits);
-	hipLaunchKernelGGL((vc_count_reads_kernel<K, W64>), dim3(grid), dim3(VC_BLOCK), lds, st, *A);
+	hipLaunchKernelGGL((vc_count_reads_kernel<K, W64, ABL>), dim3(grid), dim3(VC_BLOCK), lds, st, *A);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return e;
 	hipLaunchKernelGGL((vc_count_long_kernel<K, W64>), dim3(grid_long), dim3(VC_BLOCK), lds, st, *A);
 	return hipGetLastError();
 }
 
+#ifdef VC_ABLATION
+#define VC_ABL_LIST(X) X(1) X(2) X(4) X(8) X(3) X(6) X(7) X(10)
+#endif
+
 template <int K>
 static hipError_t launch_k(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
 {
+#ifdef VC_ABLATION
+	if (K == 21 && A->ablate && A->filter_w == VC_FILTER_W32) {
+		switch (A->ablate) {
+#define VC_ABL_CASE(n) case n: return launch_kw<21, false, n>(A, grid, grid_long, st);
+			VC_ABL_LIST(VC_ABL_CASE)
+#undef VC_ABL_CASE
+		default: break;
+		}
+	}
+#endif
 	return A->filter_w == VC_FILTER_W64 ? launch_kw<K, true>(A, grid, grid_long, st)
 	                                    : launch_kw<K, false>(A, grid, grid_long, st);
 }
@@ -583,7 +838,18 @@ template <int K>
 static hipError_t setup_k(int lds)
 {
 	hipError_t e = setup_kw<K, true>(lds);
-	return e == hipSuccess ? setup_kw<K, false>(lds) : e;
+	if (e == hipSuccess) e = setup_kw<K, false>(lds);
+#ifdef VC_ABLATION
+	if (K == 21) {
+#define VC_ABL_SET(n)                                                                           \
+	if (e == hipSuccess)                                                                        \
+		e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<21, false, n>,              \
+		                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+		VC_ABL_LIST(VC_ABL_SET)
+#undef VC_ABL_SET
+	}
+#endif
+	return e;
 }
 
 extern "C" hipError_t vc_kernel_setup(void)
