@@ -45,30 +45,29 @@ VC_HD uint64_t vc_revcomp(uint64_t x, int k)
 }
 
 /* Blocked Bloom prefilter in LDS: 2^wbits 32-bit words (wbits <= 15), two
- * bits per key inside one word.  Its hash runs once per k-mer, so it is one
- * add: fx = lo32(fwd) + lo32(revcomp), symmetric in the two strands and hence
- * a function of the canonical k-mer without computing min(fwd, rc) (the low
- * 32 bits of the two strands together cover every base of a k <= 32 k-mer).
- * Bits 0..4 pick the first bit, bits 5..19 the word, bits 20..24 the second. */
-VC_HD uint32_t vc_filter_hash(uint64_t key, int k)
+ * bits per key inside one word.  It runs once per k-mer, on the low 32 bits
+ * of the two strands, flo = lo32(fwd) and rlo = lo32(revcomp), and uses only
+ * functions symmetric in them, so it is a function of the canonical k-mer
+ * without computing min(fwd, rc):
+ *   word = bits [fsh, fsh + wbits) of lo24(flo) * lo24(rlo)   (v_mul_u32_u24)
+ *   bits = 1 << (flo & 31), 1 << (rlo & 31)                   (v_lshlrev)
+ * The bit positions are the newest and the (complemented) oldest bases of the
+ * window.  The word comes from a product because any bitwise symmetric
+ * combination (sum, xor, ...) of the two strands is constant at the bits of a
+ * self-paired base (the centre of an odd k), which left a quarter of the
+ * words empty; the product's middle bits mix all 48 input bits. */
+VC_HD uint32_t vc_filter_shift(int k, uint32_t wbits)
 {
-	return (uint32_t)key + (uint32_t)vc_revcomp(key, k);
+	/* the product has 4k significant bits; skip its skewed top 4 */
+	const int top = 4 * k - 4 < 32 ? 4 * k - 4 : 32;
+	return top > (int)wbits ? (uint32_t)(top - (int)wbits) : 0u;
 }
-/* Second symmetric hash (XOR instead of ADD) for extra filter bits. */
-VC_HD uint32_t vc_filter_hash2(uint64_t key, int k)
+VC_HD uint32_t vc_filter_mix(uint32_t flo, uint32_t rlo) { return (flo & 0xFFFFFFu) * (rlo & 0xFFFFFFu); }
+VC_HD uint32_t vc_filter_word(uint32_t flo, uint32_t rlo, uint32_t fsh, uint32_t wbits)
 {
-	return (uint32_t)key ^ (uint32_t)vc_revcomp(key, k);
+	return (vc_filter_mix(flo, rlo) >> fsh) & ((1u << wbits) - 1u);
 }
-VC_HD uint32_t vc_filter_word(uint32_t fx, uint32_t wbits) { return (fx >> 5) & ((1u << wbits) - 1u); }
-/* 32-bit-word filter: two bits. */
-VC_HD uint32_t vc_filter_mask(uint32_t fx) { return (1u << (fx & 31u)) | (1u << ((fx >> 20) & 31u)); }
-/* 64-bit-word filter (wbits <= 14): two bits in each half of the word. */
-VC_HD uint32_t vc_filter_mask_lo(uint32_t fx) { return (1u << (fx & 31u)) | (1u << ((fx >> 19) & 31u)); }
-VC_HD uint32_t vc_filter_mask_hi(uint32_t fx, uint32_t fy) { return (1u << ((fx >> 24) & 31u)) | (1u << (fy >> 27)); }
-
-/* Filter layouts (vc_ctx chooses one). */
-#define VC_FILTER_W32 32
-#define VC_FILTER_W64 64
+VC_HD uint32_t vc_filter_mask(uint32_t flo, uint32_t rlo) { return (1u << (flo & 31u)) | (1u << (rlo & 31u)); }
 
 /* Device key table slot: 16 bytes, one load per probe step. */
 typedef struct {

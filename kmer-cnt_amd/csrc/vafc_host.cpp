@@ -230,11 +230,11 @@ struct vc_ctx {
 	hipStream_t st = nullptr;
 	int n_cu = 256;
 	vc_slot_t *d_table = nullptr;
-	int filter_w = VC_FILTER_W64;
 	int ablate = 0;                   // kernel ablation variant (libvafc_abl.so only)
 	uint32_t tbits = 0;
 	uint32_t *d_filter = nullptr;
 	uint32_t wbits = 0;
+	uint32_t fsh = 0;
 	uint32_t *d_counts = nullptr;          // active outputs (own or bound)
 	unsigned long long *d_tally = nullptr;
 	uint32_t *own_counts = nullptr;
@@ -286,12 +286,10 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	while (((uint64_t)1 << tbits) < 2 * (uint64_t)n_keys + 2) ++tbits;
 	const uint64_t tslots = (uint64_t)1 << tbits;
 	std::vector<vc_slot_t> tab(tslots, vc_slot_t{VC_EMPTY_KEY, 0u, 0u});
-	// LDS prefilter: >= 24 bits per key, 1 KiB .. 128 KiB; 32-bit words with
-	// 2 bits per key (default) or 64-bit words with 4 bits (VAFC_FILTER=64)
-	const char *fenv = getenv("VAFC_FILTER");
-	const int filter_w = (fenv && atoi(fenv) == 64) ? VC_FILTER_W64 : VC_FILTER_W32;
+	// LDS prefilter: >= 24 bits per key, 1 KiB .. 128 KiB, 2 bits per key
 	uint32_t wbits = 8;
 	while (wbits < VC_MAX_FILTER_WBITS && ((uint64_t)32 << wbits) < 24 * (uint64_t)n_keys) ++wbits;
+	const uint32_t fsh = vc_filter_shift(k, wbits);
 	std::vector<uint32_t> fw((size_t)1 << wbits, 0);
 	uint64_t inserted = 0;
 	for (size_t i = 0; i < n_keys; ++i) {
@@ -307,20 +305,14 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 		if (dup) continue;             // first occurrence wins
 		tab[s].key = key;
 		tab[s].val = vals[i];
-		const uint32_t fx = vc_filter_hash(key, k);
-		if (filter_w == VC_FILTER_W32) {
-			fw[vc_filter_word(fx, wbits)] |= vc_filter_mask(fx);
-		} else {
-			const uint32_t w = vc_filter_word(fx, wbits - 1);
-			fw[2 * w] |= vc_filter_mask_lo(fx);
-			fw[2 * w + 1] |= vc_filter_mask_hi(fx, vc_filter_hash2(key, k));
-		}
+		const uint32_t flo = (uint32_t)key, rlo = (uint32_t)vc_revcomp(key, k);
+		fw[vc_filter_word(flo, rlo, fsh, wbits)] |= vc_filter_mask(flo, rlo);
 		++inserted;
 	}
 	c->n_keys = inserted;
 	c->tbits = tbits;
 	c->wbits = wbits;
-	c->filter_w = filter_w;
+	c->fsh = fsh;
 	c->ablate = getenv("VAFC_ABLATE") ? atoi(getenv("VAFC_ABLATE")) : 0;
 
 	int rc = VC_OK;
@@ -416,7 +408,7 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 	A.tmask = (uint32_t)(((uint64_t)1 << c->tbits) - 1);
 	A.filter = c->d_filter;
 	A.wbits = c->wbits;
-	A.filter_w = c->filter_w;
+	A.fsh = c->fsh;
 	A.ablate = c->ablate;
 	A.k = c->k;
 	A.kmask = ((uint64_t)1 << (2 * c->k)) - 1;

@@ -22,9 +22,9 @@ struct VcKernelArgs {
 	uint64_t n_reads;
 	const vc_slot_t *table;      // exact table, 2^tbits slots, key VC_EMPTY_KEY = empty
 	uint32_t tbits, tmask;
-	const uint32_t *filter;      // 2^wbits 32-bit words (2^(wbits-1) 64-bit words)
+	const uint32_t *filter;      // 2^wbits 32-bit words
 	uint32_t wbits;
-	int filter_w;                // VC_FILTER_W32 or VC_FILTER_W64
+	uint32_t fsh;                // filter word shift (vc_filter_shift)
 	int ablate;                  // ablation builds only (VAFC_ABLATE), 0 otherwise
 	int k;
 	uint64_t kmask;              // (1 << 2k) - 1

@@ -268,8 +268,6 @@ struct Roller {
 		inv = __builtin_amdgcn_alignbit(bad, inv, 1);
 	}
 	__device__ __forceinline__ bool valid() const { return inv < vthr; }
-	// prefilter hash: symmetric in the strands, so no min() per k-mer
-	__device__ __forceinline__ uint32_t fx() const { return flo + rlo; }
 };
 
 __device__ __forceinline__ uint64_t canonical_of(uint32_t flo, uint32_t fhi, uint32_t rlo, uint32_t rhi)
@@ -285,19 +283,17 @@ __device__ __forceinline__ uint64_t canonical_of(uint32_t flo, uint32_t fhi, uin
 // Lane processes chunks [c_lo, c_hi) of its read (chunk c = read positions
 // 16c..16c+15), emitting the canonical k-mers whose whole window lies in the
 // valid position range [vlo, vhi) (vlo = 0, vhi = len for a whole read).
-// Returns nothing; the wave's count of valid k-mers accumulates in `tally`
-// (wave-uniform).
+// The lane's count of valid k-mers accumulates in `tl`.
 // ABL (ablation builds only, -DVC_ABLATION; results are wrong by design):
-//   1 = no LDS filter reads, 2 = no global read-byte loads, 4 = no queue appends,
-//   8 = no filter stage at all (rolling + validity only)
-template <int K, bool W64, bool HAS_LO, int ABL = 0>
+//   1 = no LDS filter reads, 2 = no global read-byte loads, 4 = no queue appends
+template <int K, bool HAS_LO, int ABL = 0>
 __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
                                           uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
                                           int vlo, int vhi, int nit, const uint32_t *__restrict__ filt,
-                                          WaveQueue &Q, unsigned long long &tally, int lane)
+                                          WaveQueue &Q, uint32_t &tl, int lane)
 {
-	const uint32_t wbits = A.wbits;
-	const uint32_t zero_word = 1u << wbits;     // an all-zero LDS word past the filter
+	const uint32_t fsh = A.fsh;
+	const uint32_t zero_word = 1u << A.wbits;   // an all-zero LDS word past the filter
 	const int tail_c = (len & 15) ? (len >> 4) : -1;
 
 	uint64_t addr = off + 16ull * (uint64_t)c_lo;
@@ -351,41 +347,23 @@ __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t 
 #pragma unroll
 		for (int half = 0; half < 2; ++half) {
 			const uint32_t ta = half ? t2 : t0, tb = half ? t3 : t1;
-			uint32_t fl[8], fh[8], fw[8], fw2[8], fxs[8], fys[8];
+			uint32_t fl[8], fh[8], fw[8], fm[8];
 #pragma unroll
 			for (int j = 0; j < 8; ++j) {
 				const uint32_t tw = j < 4 ? ta : tb;
 				const uint32_t x = tw >> (8 * (j & 3));
 				R.push(x & 3u, x >> 2);
 				const bool valid = R.valid();
-				tally += (unsigned long long)__popcll(__ballot(valid));
-				const uint32_t fx = R.fx();
-				if constexpr (W64) {
-					const uint32_t widx = valid ? vc_filter_word(fx, wbits - 1u) : (zero_word >> 1);
-					uint2 w;
-					if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); w = make_uint2(widx, widx); }
-					else w = reinterpret_cast<const uint2 *>(filt)[widx];
-					fw[j] = w.x;
-					fw2[j] = w.y;
-					fys[j] = R.flo ^ R.rlo;
-				} else {
-					const uint32_t widx = valid ? vc_filter_word(fx, wbits) : zero_word;
-					if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); fw[j] = 0u; }
-					else fw[j] = filt[widx];
-				}
-				fxs[j] = fx;
+				tl += valid ? 1u : 0u;
+				const uint32_t widx = valid ? vc_filter_word(R.flo, R.rlo, fsh, A.wbits) : zero_word;
+				if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); fw[j] = 0u; }
+				else fw[j] = filt[widx];
+				fm[j] = vc_filter_mask(R.flo, R.rlo);
 				fl[j] = R.flo; fh[j] = R.fhi;
 			}
 #pragma unroll
 			for (int j = 0; j < 8; ++j) {
-				bool hit;
-				if constexpr (W64) {
-					const uint32_t ml = vc_filter_mask_lo(fxs[j]), mh = vc_filter_mask_hi(fxs[j], fys[j]);
-					hit = (((fw[j] & ml) ^ ml) | ((fw2[j] & mh) ^ mh)) == 0u;
-				} else {
-					const uint32_t fm = vc_filter_mask(fxs[j]);
-					hit = (fw[j] & fm) == fm;
-				}
+				const bool hit = (fw[j] & fm[j]) == fm[j];
 				const uint64_t bal = __ballot(hit);
 				if constexpr ((ABL & 4) != 0) { asm volatile("" :: "s"(bal)); }
 				else if (bal) queue_append(A, Q, bal, hit, ((uint64_t)fh[j] << 32) | fl[j], lane);
@@ -406,10 +384,19 @@ __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t 
 //   B  big-endian codes,    base j at bits 2(15-j)      (pair-reversed L)
 // The forward k-mer's low 32 bits at base j are one v_alignbit of (B[c-1]:B[c])
 // and the reverse complement's low 32 bits one v_alignbit of the C stream, with
-// compile-time shifts; the prefilter hash fx = lo32(fwd) + lo32(rc) needs
-// nothing else.  Hits set bits of a per-lane 16-bit mask; only at the end of a
-// chunk, and only if some lane of the wave has a hit, are the full forward
-// k-mers of the hit positions extracted (variable shift) and queued.
+// compile-time shifts; the prefilter needs nothing else.  Filter passes set
+// bits of a per-lane 16-bit mask hm (bit 15-j <-> window ending at base j).
+//
+// Window validity is not tracked per base: per chunk, V (same bit order as
+// hm) holds the windows that lie inside [vlo, vhi) and contain no invalid
+// base; hm &= V.  Windows ending at base j are valid iff j >= L + K - 16c
+// (L = last invalid position before the chunk, vlo - 1 at the start) and
+// 16c + j < vhi; U = 16 - (L + K - 16c) and Qe = 16 - (vhi - 16c) are carried
+// per lane.  A chunk with an invalid base of its own (an N; rare) also
+// invalidates its windows from the first such base on and moves L to the last.
+// Only at the end of a chunk, and only if some lane of the wave has a hit,
+// are the full forward k-mers of the hit positions extracted (variable
+// shift) and queued.
 
 // 4x4 transpose of 2-bit fields: (byte r, field c) <-> (byte c, field r).
 __device__ __forceinline__ uint32_t transpose2x4x4(uint32_t a)
@@ -428,17 +415,18 @@ __device__ __forceinline__ uint32_t pairrev(uint32_t x)
 	return ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
 }
 
-template <int K, bool W64, bool HAS_LO, int ABL = 0>
+__device__ __forceinline__ int clamp16(int v) { return v < 0 ? 0 : (v > 16 ? 16 : v); }
+
+template <int K, bool HAS_LO, int ABL = 0>
 __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
                                                  uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
                                                  int vlo, int vhi, int nit,
                                                  const uint32_t *__restrict__ filt, WaveQueue &Q,
-                                                 unsigned long long &tally, int lane)
+                                                 uint32_t &tl, int lane)
 {
 	static_assert(K >= 17 && K <= 31, "packed scan needs 17 <= k <= 31");
 	constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
-	constexpr uint32_t VTHR = 1u << (32 - K);
-	const uint32_t wbits = A.wbits;
+	const uint32_t fsh = A.fsh;
 	const int tail_c = (len & 15) ? (len >> 4) : -1;
 
 	uint64_t addr = off + 16ull * (uint64_t)c_lo;
@@ -453,7 +441,8 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	if (c_lo + 1 < c_hi) ld4(s32, wi + 5, wmax, x1, x2, x3, x4);
 
 	uint32_t Bm1 = 0, Bm2 = 0, Cm1 = 0, Cm2 = 0;   // streams of the two previous chunks
-	uint32_t inv = 0xFFFFFFFFu;                     // invalid flags, newest in bit 31
+	int U = 1 - K - vlo + 16 * c_lo;                 // +16 at the top of every chunk
+	int Qe = -vhi + 16 * c_lo;
 
 	for (int it = 0; it < nit; ++it) {
 		const int c = c_lo + it;
@@ -473,21 +462,8 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 		if (__ballot(c == tail_c)) {
 			if (c == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
 		}
-		const int P = 16 * c;
-		if (__ballot(P + 16 > vhi)) {
-			t0 |= range_mask_hi(vhi - P);
-			t1 |= range_mask_hi(vhi - P - 4);
-			t2 |= range_mask_hi(vhi - P - 8);
-			t3 |= range_mask_hi(vhi - P - 12);
-		}
-		if (HAS_LO) {
-			if (__ballot(P < vlo)) {
-				t0 |= range_mask_lo(vlo - P);
-				t1 |= range_mask_lo(vlo - P - 4);
-				t2 |= range_mask_lo(vlo - P - 8);
-				t3 |= range_mask_lo(vlo - P - 12);
-			}
-		}
+		U += 16;
+		Qe += 16;
 		// pack the chunk's codes: byte r of A holds bases r, 4+r, 8+r, 12+r
 		const uint32_t Am = (t0 & 0x03030303u) | ((t1 & 0x03030303u) << 2) |
 		                    ((t2 & 0x03030303u) << 4) | ((t3 & 0x03030303u) << 6);
@@ -495,58 +471,46 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 		const uint32_t Cc = ~L;                          // complement codes, little-endian
 		const uint32_t Bc = pairrev(L);                  // big-endian codes
 
-		uint32_t hm = 0;                                 // hit bit (15 - j) for base j
+		uint32_t hm = 0;                                 // filter pass, bit 15 - j for base j
+		uint32_t fw[16], fm[16];
 #pragma unroll
-		for (int half = 0; half < 2; ++half) {
-			const uint32_t ta = half ? t2 : t0, tb = half ? t3 : t1;
-			uint32_t fw[8], fxs[8], fw2[8], fys[8];
-			uint64_t vld[8];                             // valid windows, one wave mask per base
+		for (int j = 0; j < 16; ++j) {
+			const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, (uint32_t)(2 * (15 - j)));
+			const int s2 = j - K + 1 + 32;               // window start relative to chunk c-2
+			uint32_t rlo;
+			if (s2 >= 16) rlo = __builtin_amdgcn_alignbit(Cc, Cm1, (uint32_t)(2 * (s2 - 16)));
+			else rlo = __builtin_amdgcn_alignbit(Cm1, Cm2, (uint32_t)(2 * s2));
+			const uint32_t widx = vc_filter_mix(flo, rlo) >> fsh;   // < 2^wbits: fsh = 32 - wbits for k >= 9
+			if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); fw[j] = widx; }
+			else fw[j] = filt[widx];
+			fm[j] = vc_filter_mask(flo, rlo);
+		}
 #pragma unroll
-			for (int jj = 0; jj < 8; ++jj) {
-				const int j = half * 8 + jj;
-				const uint32_t tw = jj < 4 ? ta : tb;
-				inv = __builtin_amdgcn_alignbit(tw >> (8 * (j & 3) + 2), inv, 1);
-				vld[jj] = __ballot(inv < VTHR);
-				tally += (unsigned long long)__popcll(vld[jj]);   // wave-uniform, SALU
-				const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, (uint32_t)(2 * (15 - j)));
-				const int s2 = j - K + 1 + 32;             // window start relative to chunk c-2
-				uint32_t rlo;
-				if (s2 >= 16) rlo = __builtin_amdgcn_alignbit(Cc, Cm1, (uint32_t)(2 * (s2 - 16)));
-				else rlo = __builtin_amdgcn_alignbit(Cm1, Cm2, (uint32_t)(2 * s2));
-				const uint32_t fx = flo + rlo;
-				// invalid windows read some filter word; their hits are masked below
-				if constexpr (W64) {
-					const uint32_t widx = vc_filter_word(fx, wbits - 1u);
-					uint2 w;
-					if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); w = make_uint2(widx, widx); }
-					else w = reinterpret_cast<const uint2 *>(filt)[widx];
-					fw[jj] = w.x;
-					fw2[jj] = w.y;
-					fys[jj] = flo ^ rlo;
-				} else {
-					const uint32_t widx = vc_filter_word(fx, wbits);
-					if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); fw[jj] = 0u; }
-					else fw[jj] = filt[widx];
-				}
-				fxs[jj] = fx;
-			}
-#pragma unroll
-			for (int jj = 0; jj < 8; ++jj) {
-				bool pass;
-				if constexpr (W64) {
-					const uint32_t ml = vc_filter_mask_lo(fxs[jj]), mh = vc_filter_mask_hi(fxs[jj], fys[jj]);
-					pass = (((fw[jj] & ml) ^ ml) | ((fw2[jj] & mh) ^ mh)) == 0u;
-				} else {
-					const uint32_t fm = vc_filter_mask(fxs[jj]);
-					pass = (fw[jj] & fm) == fm;
-				}
-				// hm = 2*hm + hit with the hit wave mask as carry-in: one v_addc
-				const uint64_t hb = __ballot(pass) & vld[jj];
-				uint64_t cout;
-				asm volatile("v_addc_co_u32 %0, %1, %2, %2, %3" : "=v"(hm), "=s"(cout) : "v"(hm), "s"(hb));
-				(void)cout;
+		for (int j = 0; j < 16; ++j) {
+			// hm = 2*hm + pass with the pass wave mask as carry-in: one v_addc
+			const uint64_t pb = __ballot((~fw[j] & fm[j]) == 0u);
+			uint64_t cout;
+			asm volatile("v_addc_co_u32 %0, %1, %2, %2, %3" : "=v"(hm), "=s"(cout) : "v"(hm), "s"(pb));
+			(void)cout;
+		}
+		// windows of this chunk inside [vlo, vhi) with no earlier invalid base
+		uint32_t V = ((1u << clamp16(U)) - 1u) & ~((1u << clamp16(Qe)) - 1u);
+		const uint32_t anyinv = (t0 | t1 | t2 | t3) & 0x04040404u;
+		if (__ballot(anyinv != 0u)) {
+			if (anyinv != 0u) {
+				// invalid flags packed like the codes: base j at bit 2j of F
+				const uint32_t Im = ((t0 >> 2) & 0x01010101u) | (t1 & 0x04040404u) |
+				                    ((t2 << 2) & 0x10101010u) | ((t3 << 4) & 0x40404040u);
+				const uint32_t F = transpose2x4x4(Im);
+				const int j0 = (int)((uint32_t)__builtin_ctz(F) >> 1);          // first invalid base
+				const int j1 = (int)((31u - (uint32_t)__builtin_clz(F)) >> 1);  // last invalid base
+				V &= ~((2u << (15 - j0)) - 1u);          // windows ending at j >= j0
+				const int u1 = 16 - j1 - K;
+				U = U < u1 ? U : u1;
 			}
 		}
+		hm &= V;
+		tl += (uint32_t)__builtin_popcount(V);
 		// queue the hit positions' forward k-mers (bit b <-> base j = 15 - b)
 		if constexpr ((ABL & 4) != 0) {
 			asm volatile("" :: "v"(hm));
@@ -572,18 +536,16 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 
 // k in 17..31 with a compile-time specialisation: packed streams; otherwise
 // the general rolling scan.
-template <int K, bool W64, bool HAS_LO, int ABL = 0>
+template <int K, bool HAS_LO, int ABL = 0>
 __device__ __forceinline__ void scan_any(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
                                          uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
                                          int vlo, int vhi, int nit, const uint32_t *__restrict__ filt,
-                                         WaveQueue &Q, unsigned long long &tally, int lane)
+                                         WaveQueue &Q, uint32_t &tl, int lane)
 {
 	if constexpr (K >= 17)
-		scan_span_packed<K, W64, HAS_LO, ABL>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q,
-		                                       tally, lane);
+		scan_span_packed<K, HAS_LO, ABL>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl, lane);
 	else
-		scan_span<K, W64, HAS_LO, ABL>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tally,
-		                               lane);
+		scan_span<K, HAS_LO, ABL>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl, lane);
 }
 
 __device__ __forceinline__ void load_filter(const VcKernelArgs &A, uint32_t *filt)
@@ -600,7 +562,7 @@ __device__ __forceinline__ void load_filter(const VcKernelArgs &A, uint32_t *fil
 // kernel 1: whole reads, one lane per read
 // ---------------------------------------------------------------------------
 
-template <int K, bool W64, int ABL = 0>
+template <int K, int ABL = 0>
 __global__ void __launch_bounds__(VC_BLOCK)
 vc_count_reads_kernel(VcKernelArgs A)
 {
@@ -632,11 +594,13 @@ vc_count_reads_kernel(VcKernelArgs A)
 		}
 		const int nch = (len + 15) >> 4;
 		const int nit = wave_max_i32(nch);
-		scan_any<K, W64, false, ABL>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tally, lane);
+		uint32_t tl = 0;
+		scan_any<K, false, ABL>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tl, lane);
+		tally += tl;
 		queue_flush(A, Q, lane);     // one drain per read group, probes overlapped
 	}
 	queue_flush(A, Q, lane);
-	const unsigned long long t = tally;      // wave-uniform count
+	const unsigned long long t = wave_sum_u64(tally);
 	if (lane == 0 && t) atomicAdd(A.tally, t);
 }
 
@@ -644,7 +608,7 @@ vc_count_reads_kernel(VcKernelArgs A)
 // kernel 2: long reads, every lane of the grid takes one segment
 // ---------------------------------------------------------------------------
 
-template <int K, bool W64>
+template <int K>
 __global__ void __launch_bounds__(VC_BLOCK)
 vc_count_long_kernel(VcKernelArgs A)
 {
@@ -683,11 +647,13 @@ vc_count_long_kernel(VcKernelArgs A)
 				c_hi = (vhi + 15) >> 4;
 			}
 			const int nit = wave_max_i32(c_hi - c_lo);
-			scan_any<K, W64, true>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tally, lane);
+			uint32_t tl = 0;
+			scan_any<K, true>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl, lane);
+			tally += tl;
 		}
 	}
 	queue_flush(A, Q, lane);
-	const unsigned long long t = tally;      // wave-uniform count
+	const unsigned long long t = wave_sum_u64(tally);
 	if (lane == 0 && t) atomicAdd(A.tally, t);
 }
 
@@ -783,36 +749,35 @@ __global__ void vc_synth_kernel(uint8_t *seq, uint64_t *offs, uint32_t *lens, ui
 // launchers
 // ---------------------------------------------------------------------------
 
-template <int K, bool W64, int ABL = 0>
+template <int K, int ABL = 0>
 static hipError_t launch_kw(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
 {
 	const size_t lds = vc_lds_bytes(A->wbits);
-	hipLaunchKernelGGL((vc_count_reads_kernel<K, W64, ABL>), dim3(grid), dim3(VC_BLOCK), lds, st, *A);
+	hipLaunchKernelGGL((vc_count_reads_kernel<K, ABL>), dim3(grid), dim3(VC_BLOCK), lds, st, *A);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return e;
-	hipLaunchKernelGGL((vc_count_long_kernel<K, W64>), dim3(grid_long), dim3(VC_BLOCK), lds, st, *A);
+	hipLaunchKernelGGL((vc_count_long_kernel<K>), dim3(grid_long), dim3(VC_BLOCK), lds, st, *A);
 	return hipGetLastError();
 }
 
 #ifdef VC_ABLATION
-#define VC_ABL_LIST(X) X(1) X(2) X(4) X(8) X(3) X(6) X(7) X(10)
+#define VC_ABL_LIST(X) X(1) X(2) X(4) X(3) X(5) X(6) X(7)
 #endif
 
 template <int K>
 static hipError_t launch_k(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
 {
 #ifdef VC_ABLATION
-	if (K == 21 && A->ablate && A->filter_w == VC_FILTER_W32) {
+	if (K == 21 && A->ablate) {
 		switch (A->ablate) {
-#define VC_ABL_CASE(n) case n: return launch_kw<21, false, n>(A, grid, grid_long, st);
+#define VC_ABL_CASE(n) case n: return launch_kw<21, n>(A, grid, grid_long, st);
 			VC_ABL_LIST(VC_ABL_CASE)
 #undef VC_ABL_CASE
 		default: break;
 		}
 	}
 #endif
-	return A->filter_w == VC_FILTER_W64 ? launch_kw<K, true>(A, grid, grid_long, st)
-	                                    : launch_kw<K, false>(A, grid, grid_long, st);
+	return launch_kw<K>(A, grid, grid_long, st);
 }
 
 extern "C" hipError_t vc_launch_count(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
@@ -824,26 +789,19 @@ extern "C" hipError_t vc_launch_count(const VcKernelArgs *A, int grid, int grid_
 	}
 }
 
-template <int K, bool W64>
-static hipError_t setup_kw(int lds)
-{
-	hipError_t e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<K, W64>,
-	                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-	if (e != hipSuccess) return e;
-	return hipFuncSetAttribute((const void *)vc_count_long_kernel<K, W64>,
-	                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-}
-
 template <int K>
 static hipError_t setup_k(int lds)
 {
-	hipError_t e = setup_kw<K, true>(lds);
-	if (e == hipSuccess) e = setup_kw<K, false>(lds);
+	hipError_t e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<K>,
+	                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+	if (e == hipSuccess)
+		e = hipFuncSetAttribute((const void *)vc_count_long_kernel<K>,
+		                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 #ifdef VC_ABLATION
 	if (K == 21) {
 #define VC_ABL_SET(n)                                                                           \
 	if (e == hipSuccess)                                                                        \
-		e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<21, false, n>,              \
+		e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<21, n>,                     \
 		                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 		VC_ABL_LIST(VC_ABL_SET)
 #undef VC_ABL_SET

@@ -207,8 +207,10 @@ def test_device_generator_matches_numpy(torch_dev):
         assert np.all(d_lens.cpu().numpy() == L)
 
 
-def test_device_resident_unaligned_and_filters(torch_dev):
-    """count_device on HBM reads at every byte misalignment, both LDS filter layouts."""
+@pytest.mark.parametrize("k", [21, 31, 25, 13])
+def test_device_resident_unaligned(torch_dev, k):
+    """count_device on HBM reads at every byte misalignment; compile-time k (21, 31:
+    packed streams) and run-time k (25, 13: rolling scan)."""
     import torch
     import vafc
     import vafc_synth as S
@@ -217,32 +219,27 @@ def test_device_resident_unaligned_and_filters(torch_dev):
     panel = S.make_panel(S.synthetic_bed(3000))
     with tempfile.TemporaryDirectory() as d:
         pat = os.path.join(d, "p.txt")
-        panel.write_patterns(pat, 21)
+        panel.write_patterns(pat, k)
         db = vafc.load_patterns(pat)
-        keys, vals, _ = db.keys(21)
+        keys, vals, _ = db.keys(k)
         reads = S.gen_reads(panel, 20000, f_snp=0.5)
         seq, offs, lens = S.pack_reads(reads)
-        want, km_want = O.Oracle(21, pattern_fn=pat).count_reads(seq, offs, lens)
+        want, km_want = O.Oracle(k, pattern_fn=pat).count_reads(seq, offs, lens)
+    m = vafc.KmerMap(k, keys, vals, db.n, 0)
     res = []
-    for fw in ("64", "32"):
-        os.environ["VAFC_FILTER"] = fw
-        try:
-            m = vafc.KmerMap(21, keys, vals, db.n, 0)
-        finally:
-            os.environ.pop("VAFC_FILTER", None)
-        for mis in range(4):
-            buf = torch.zeros(seq.size + 8, dtype=torch.uint8, device=torch_dev)
-            buf[mis:mis + seq.size] = torch.from_numpy(seq).to(torch_dev)
-            d_offs = torch.from_numpy(offs.astype(np.int64)).to(torch_dev)
-            d_lens = torch.from_numpy(lens.astype(np.int32)).to(torch_dev)
-            torch.cuda.synchronize()
-            m.reset()
-            m.count_device(buf.data_ptr() + mis, seq.size, d_offs.data_ptr(), d_lens.data_ptr(), lens.size)
-            got, km = m.finish()
-            assert km == km_want, (fw, mis)
-            assert np.array_equal(got, want), (fw, mis)
-            res.append(int(got.sum()))
-        m.close()
+    for mis in range(4):
+        buf = torch.zeros(seq.size + 8, dtype=torch.uint8, device=torch_dev)
+        buf[mis:mis + seq.size] = torch.from_numpy(seq).to(torch_dev)
+        d_offs = torch.from_numpy(offs.astype(np.int64)).to(torch_dev)
+        d_lens = torch.from_numpy(lens.astype(np.int32)).to(torch_dev)
+        torch.cuda.synchronize()
+        m.reset()
+        m.count_device(buf.data_ptr() + mis, seq.size, d_offs.data_ptr(), d_lens.data_ptr(), lens.size)
+        got, km = m.finish()
+        assert km == km_want, mis
+        assert np.array_equal(got, want), mis
+        res.append(int(got.sum()))
+    m.close()
     assert min(res) > 0
 
 

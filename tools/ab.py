@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of counter variants in ONE process (same device, same
 HBM-resident reads): variants differ by environment knobs read at vc_create
-time (e.g. VAFC_FILTER=32|64).  Also checks that every variant produces the
+time (e.g. VAFC_ABLATE=0|4 with the ablation build).  Also checks that every variant produces the
 same counts.  Usage (GPU box):
-    python tools/ab.py --reads 100000000 --rounds 10 VAFC_FILTER=64 VAFC_FILTER=32
+    VAFC_LIB=kmer-cnt_amd/lib/libvafc_abl.so python tools/ab.py --rounds 10 VAFC_ABLATE=0 VAFC_ABLATE=4
 """
 import argparse
 import os

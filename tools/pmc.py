@@ -66,7 +66,23 @@ def main():
         derived["hbm_bytes_per_launch"] = sum(derived.values())
     with open(os.path.join(out, "pmc_counters.json"), "w") as f:
         json.dump({"kernel": KERNEL, "bench_args": bench_args, "counters": acc, "derived": derived}, f, indent=1)
+    # the summary bench.py reads for roofline.traffic (same workload only)
+    if "hbm_bytes_per_launch" in derived:
+        summ = {"kernel": KERNEL, "reads": _arg(bench_args, "--reads", 100_000_000),
+                "read_len": _arg(bench_args, "--read-len", 150), "k": _arg(bench_args, "--k", 21),
+                "hbm_bytes_per_launch": derived["hbm_bytes_per_launch"],
+                "hbm_read_bytes_per_launch": derived.get("hbm_read_bytes_per_launch"),
+                "hbm_write_bytes_per_launch": derived.get("hbm_write_bytes_per_launch"),
+                "fetch_size_kib_raw": acc.get("FETCH_SIZE"),
+                "correction": "read bytes = FETCH_SIZE x 1024 x 2 (gfx950 tallies 128-B requests at 64 B)",
+                "counters": acc}
+        with open(os.path.join(out, "pmc_summary.json"), "w") as f:
+            json.dump(summ, f, indent=1)
     print(json.dumps(derived))
+
+
+def _arg(args, name, default):
+    return int(args[args.index(name) + 1]) if name in args else default
 
 
 if __name__ == "__main__":
