@@ -240,6 +240,7 @@ struct vc_ctx {
 	uint32_t *own_counts = nullptr;
 	unsigned long long *own_tally = nullptr;
 	uint32_t *d_nlong = nullptr;
+	uint8_t *d_pad = nullptr;              // 64 B staging for inputs under 16 B (kernels load 16 B)
 	uint32_t *d_long = nullptr;
 	uint32_t long_cap = 0;
 	Slot slot[2];
@@ -333,6 +334,8 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	c->d_counts = c->own_counts;
 	c->d_tally = c->own_tally;
 	TRY(hipMalloc(&c->d_nlong, sizeof(uint32_t)));
+	TRY(hipMalloc(&c->d_pad, 64));
+	TRY(hipMemset(c->d_pad, 0, 64));
 	TRY(hipMemcpy(c->d_table, tab.data(), tslots * sizeof(vc_slot_t), hipMemcpyHostToDevice));
 	TRY(hipMemcpy(c->d_filter, fw.data(), fw.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
 	TRY(hipMemset(c->d_counts, 0, (2 * (size_t)n_patterns + 2) * sizeof(uint32_t)));
@@ -383,6 +386,7 @@ extern "C" void vc_destroy(vc_ctx *c)
 	if (c->own_counts) (void)hipFree(c->own_counts);
 	if (c->own_tally) (void)hipFree(c->own_tally);
 	if (c->d_nlong) (void)hipFree(c->d_nlong);
+	if (c->d_pad) (void)hipFree(c->d_pad);
 	if (c->d_long) (void)hipFree(c->d_long);
 	if (c->st) (void)hipStreamDestroy(c->st);
 	delete c;
@@ -400,6 +404,13 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 	A.seq = (const uint8_t *)(p & ~(uintptr_t)3);
 	A.off_adj = (uint64_t)(p & 3u);
 	A.seq_words = (seq_bytes + A.off_adj + 3) / 4;
+	const bool tiny = A.seq_words < 4;     // the scan loads whole 16-byte quads
+	if (tiny) {
+		HIPCK(hipMemcpyAsync(c->d_pad, d_seq, seq_bytes, hipMemcpyDeviceToDevice, st));
+		A.seq = c->d_pad;
+		A.off_adj = 0;
+		A.seq_words = 16;
+	}
 	A.offs = d_offs;
 	A.lens = d_lens;
 	A.n_reads = n_reads;
@@ -422,6 +433,7 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 	HIPCK(hipMemsetAsync(c->d_nlong, 0, sizeof(uint32_t), st));
 	if (c->timing) HIPCK(hipEventRecord(c->t0, st));
 	HIPCK(vc_launch_count(&A, grid, c->n_cu, st));
+	if (tiny) HIPCK(hipStreamSynchronize(st));   // d_pad is reused by the next tiny call
 	if (c->timing) {
 		HIPCK(hipEventRecord(c->t1, st));
 		c->timed = true;
