@@ -37,14 +37,17 @@
 // small helpers
 // ---------------------------------------------------------------------------
 
+// Wave maximum of a small non-negative value (< 2048) from 11 ballots: no
+// cross-lane data movement, so no LDS round trips.
 __device__ __forceinline__ int wave_max_i32(int v)
 {
+	int m = 0;
 #pragma unroll
-	for (int o = 32; o > 0; o >>= 1) {
-		int u = __shfl_xor(v, o, WAVE);
-		v = u > v ? u : v;
+	for (int b = 10; b >= 0; --b) {
+		const int t = m | (1 << b);
+		if (__ballot(v >= t)) m = t;
 	}
-	return v;
+	return m;
 }
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
@@ -210,6 +213,9 @@ __device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q
 	if (Q.n > VC_QCAP - WAVE) {
 		drain_range(A, Q.q, Q.n - WAVE, Q.n, lane);
 		Q.n -= WAVE;
+		// leave nothing in flight on this (rare) path, so that the compiler
+		// can keep counting the scan's prefetches across it
+		__builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
 	}
 }
 
@@ -417,6 +423,129 @@ __device__ __forceinline__ uint32_t pairrev(uint32_t x)
 
 __device__ __forceinline__ int clamp16(int v) { return v < 0 ? 0 : (v > 16 ? 16 : v); }
 
+// One 16-base chunk c of the packed scan from its five dwords (w0: the dword
+// holding the chunk's first byte, realigned by sh); (B1, C1) / (B2, C2) are
+// the streams of chunks c-1 / c-2 and move on to c / c-1.
+template <int K, int ABL>
+__device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int tail_c, uint32_t sh,
+                                             uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
+                                             uint32_t &Bm1, uint32_t &Bm2, uint32_t &Cm1, uint32_t &Cm2,
+                                             int &U, int &Qe, const uint32_t *__restrict__ filt, WaveQueue &Q,
+                                             uint32_t &tl, int lane)
+{
+	constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
+	const uint32_t fsh = A.fsh;
+	const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+	const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+	const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+	const uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
+	uint32_t t0 = dec_head(b0), t1 = dec_head(b1), t2 = dec_head(b2), t3 = dec_head(b3);
+	if (__ballot(c == tail_c)) {
+		if (c == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
+	}
+	U += 16;
+	Qe += 16;
+	// pack the chunk's codes: byte r of A holds bases r, 4+r, 8+r, 12+r
+	const uint32_t Am = (t0 & 0x03030303u) | ((t1 & 0x03030303u) << 2) |
+	                    ((t2 & 0x03030303u) << 4) | ((t3 & 0x03030303u) << 6);
+	const uint32_t L = transpose2x4x4(Am);          // base j at bits 2j
+	const uint32_t Cc = ~L;                          // complement codes, little-endian
+	const uint32_t Bc = pairrev(L);                  // big-endian codes
+
+	uint32_t hm = 0;                                 // filter pass, bit 15 - j for base j
+	uint32_t fw[16], fm[16];
+#pragma unroll
+	for (int j = 0; j < 16; ++j) {
+		const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, (uint32_t)(2 * (15 - j)));
+		const int s2 = j - K + 1 + 32;               // window start relative to chunk c-2
+		uint32_t rlo;
+		if (s2 >= 16) rlo = __builtin_amdgcn_alignbit(Cc, Cm1, (uint32_t)(2 * (s2 - 16)));
+		else rlo = __builtin_amdgcn_alignbit(Cm1, Cm2, (uint32_t)(2 * s2));
+		const uint32_t widx = vc_filter_mix(flo, rlo) >> fsh;   // < 2^wbits: fsh = 32 - wbits for k >= 9
+		if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); fw[j] = widx; }
+		else fw[j] = filt[widx];
+		fm[j] = vc_filter_mask(flo, rlo);
+	}
+#pragma unroll
+	for (int j = 0; j < 16; ++j) {
+		// hm = 2*hm + pass with the pass wave mask as carry-in: one v_addc
+		const uint64_t pb = __ballot((~fw[j] & fm[j]) == 0u);
+		uint64_t cout;
+		asm volatile("v_addc_co_u32 %0, %1, %2, %2, %3" : "=v"(hm), "=s"(cout) : "v"(hm), "s"(pb));
+		(void)cout;
+	}
+	// windows of this chunk inside [vlo, vhi) with no earlier invalid base
+	uint32_t V = ((1u << clamp16(U)) - 1u) & ~((1u << clamp16(Qe)) - 1u);
+	const uint32_t anyinv = (t0 | t1 | t2 | t3) & 0x04040404u;
+	if (__ballot(anyinv != 0u)) {
+		if (anyinv != 0u) {
+			// invalid flags packed like the codes: base j at bit 2j of F
+			const uint32_t Im = ((t0 >> 2) & 0x01010101u) | (t1 & 0x04040404u) |
+			                    ((t2 << 2) & 0x10101010u) | ((t3 << 4) & 0x40404040u);
+			const uint32_t F = transpose2x4x4(Im);
+			const int j0 = (int)((uint32_t)__builtin_ctz(F) >> 1);          // first invalid base
+			const int j1 = (int)((31u - (uint32_t)__builtin_clz(F)) >> 1);  // last invalid base
+			V &= ~((2u << (15 - j0)) - 1u);          // windows ending at j >= j0
+			const int u1 = 16 - j1 - K;
+			U = U < u1 ? U : u1;
+		}
+	}
+	hm &= V;
+	tl += (uint32_t)__builtin_popcount(V);
+	// queue the hit positions' forward k-mers (bit b <-> base j = 15 - b)
+	if constexpr ((ABL & 4) != 0) {
+		asm volatile("" :: "v"(hm));
+	} else if (__ballot(hm != 0u)) {
+		for (;;) {
+			const bool has = hm != 0u;
+			const uint64_t bal = __ballot(has);
+			if (!bal) break;
+			const uint32_t b = has ? 31u - (uint32_t)__builtin_clz(hm) : 0u;
+			const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, 2u * b);
+			const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
+			queue_append(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
+			hm &= ~(1u << b);
+		}
+	}
+	Bm2 = Bm1; Bm1 = Bc;
+	Cm2 = Cm1; Cm1 = Cc;
+}
+
+// One global_load_dwordx4 of dwords [q, q+4), always exactly one load
+// instruction, so that the compiler can count loads in flight and wait only
+// for the quad a chunk is about to use.  A quad that would pass the end of
+// the buffer is loaded from its last four dwords instead (the host guarantees
+// at least four) and the return value says how far it was moved back; the
+// user shifts the dwords into place (quad_fix).  Dwords past the end of the
+// buffer are never part of a read.
+__device__ __forceinline__ uint32_t ldq(const uint32_t *__restrict__ s32, uint64_t q, uint64_t wmax,
+                                        uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
+{
+	const uint64_t lim = wmax - 3u;
+	const bool clamp = q > lim;
+	const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(s32 + (clamp ? lim : q));
+	a = v.x; b = v.y; c = v.z; d = v.w;
+	return clamp ? (q - lim > 3u ? 3u : (uint32_t)(q - lim)) : 0u;
+}
+
+__device__ __forceinline__ void quad_fix(uint32_t sft, uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
+{
+	if (__ballot(sft != 0u)) {       // only the last reads of a buffer
+		asm volatile("");            // keep this rare branch a branch
+		if (sft != 0u) {
+			a = sft == 1u ? b : (sft == 2u ? c : d);
+			b = sft == 1u ? c : d;
+			c = d;
+		}
+	}
+}
+
+// Chunks are processed in pairs.  The 8 dwords of the next pair are requested
+// (two dwordx4 from the same lines, back to back) while the current pair is
+// scanned, so each load has two chunks of work to hide behind.  The steady
+// loop issues the same loads on every trip (lanes past their span re-read
+// harmless bytes), the last pair is peeled: the compiler then waits for a
+// pair's data only when the pair starts.
 template <int K, bool HAS_LO, int ABL = 0>
 __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
                                                  uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
@@ -425,112 +554,49 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
                                                  uint32_t &tl, int lane)
 {
 	static_assert(K >= 17 && K <= 31, "packed scan needs 17 <= k <= 31");
-	constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
-	const uint32_t fsh = A.fsh;
 	const int tail_c = (len & 15) ? (len >> 4) : -1;
 
 	uint64_t addr = off + 16ull * (uint64_t)c_lo;
 	uint64_t wi = addr >> 2;
 	const uint32_t sh = (uint32_t)(addr & 3u);
-	uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
-	uint32_t x1 = 0, x2 = 0, x3 = 0, x4 = 0;
-	if (c_lo < c_hi) {
-		ld4(s32, wi, wmax, w0, w1, w2, w3);
-		w4 = ldw(s32, wi + 4, wmax);
-	}
-	if (c_lo + 1 < c_hi) ld4(s32, wi + 5, wmax, x1, x2, x3, x4);
+	uint32_t w0, w1, w2, w3, w4, w5, w6, w7, w8;
+	w0 = ldw(s32, wi, wmax);
+	uint32_t d1 = ldq(s32, wi + 1, wmax, w1, w2, w3, w4);
+	uint32_t d5 = ldq(s32, wi + 5, wmax, w5, w6, w7, w8);
 
 	uint32_t Bm1 = 0, Bm2 = 0, Cm1 = 0, Cm2 = 0;   // streams of the two previous chunks
 	int U = 1 - K - vlo + 16 * c_lo;                 // +16 at the top of every chunk
 	int Qe = -vhi + 16 * c_lo;
 
-	for (int it = 0; it < nit; ++it) {
+	int it = 0;
+	for (; it + 2 < nit; it += 2) {
 		const int c = c_lo + it;
-		uint32_t y1 = 0, y2 = 0, y3 = 0, y4 = 0;
-		if (c + 2 < c_hi) {
-			if constexpr ((ABL & 2) != 0) {
-				y1 = (uint32_t)wi * 0x9E3779B1u; y2 = y1 ^ 0x41434754u; y3 = y1 + 0x54474341u; y4 = y1 * 5u;
-			} else {
-				ld4(s32, wi + 9, wmax, y1, y2, y3, y4);
-			}
+		uint32_t n0, n1, n2, n3, n4, n5, n6, n7, dn0, dn4;
+		if constexpr ((ABL & 2) != 0) {
+			n0 = (uint32_t)wi * 0x9E3779B1u; n1 = n0 ^ 0x41434754u; n2 = n0 + 0x54474341u; n3 = n0 * 5u;
+			n4 = n0 ^ 0x5A5A5A5Au; n5 = n1 + 7u; n6 = n2 ^ n3; n7 = n4 * 3u;
+			dn0 = dn4 = 0;
+		} else {
+			dn0 = ldq(s32, wi + 9, wmax, n0, n1, n2, n3);
+			dn4 = ldq(s32, wi + 13, wmax, n4, n5, n6, n7);
 		}
-		const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
-		const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
-		const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
-		const uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
-		uint32_t t0 = dec_head(b0), t1 = dec_head(b1), t2 = dec_head(b2), t3 = dec_head(b3);
-		if (__ballot(c == tail_c)) {
-			if (c == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
-		}
-		U += 16;
-		Qe += 16;
-		// pack the chunk's codes: byte r of A holds bases r, 4+r, 8+r, 12+r
-		const uint32_t Am = (t0 & 0x03030303u) | ((t1 & 0x03030303u) << 2) |
-		                    ((t2 & 0x03030303u) << 4) | ((t3 & 0x03030303u) << 6);
-		const uint32_t L = transpose2x4x4(Am);          // base j at bits 2j
-		const uint32_t Cc = ~L;                          // complement codes, little-endian
-		const uint32_t Bc = pairrev(L);                  // big-endian codes
-
-		uint32_t hm = 0;                                 // filter pass, bit 15 - j for base j
-		uint32_t fw[16], fm[16];
-#pragma unroll
-		for (int j = 0; j < 16; ++j) {
-			const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, (uint32_t)(2 * (15 - j)));
-			const int s2 = j - K + 1 + 32;               // window start relative to chunk c-2
-			uint32_t rlo;
-			if (s2 >= 16) rlo = __builtin_amdgcn_alignbit(Cc, Cm1, (uint32_t)(2 * (s2 - 16)));
-			else rlo = __builtin_amdgcn_alignbit(Cm1, Cm2, (uint32_t)(2 * s2));
-			const uint32_t widx = vc_filter_mix(flo, rlo) >> fsh;   // < 2^wbits: fsh = 32 - wbits for k >= 9
-			if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); fw[j] = widx; }
-			else fw[j] = filt[widx];
-			fm[j] = vc_filter_mask(flo, rlo);
-		}
-#pragma unroll
-		for (int j = 0; j < 16; ++j) {
-			// hm = 2*hm + pass with the pass wave mask as carry-in: one v_addc
-			const uint64_t pb = __ballot((~fw[j] & fm[j]) == 0u);
-			uint64_t cout;
-			asm volatile("v_addc_co_u32 %0, %1, %2, %2, %3" : "=v"(hm), "=s"(cout) : "v"(hm), "s"(pb));
-			(void)cout;
-		}
-		// windows of this chunk inside [vlo, vhi) with no earlier invalid base
-		uint32_t V = ((1u << clamp16(U)) - 1u) & ~((1u << clamp16(Qe)) - 1u);
-		const uint32_t anyinv = (t0 | t1 | t2 | t3) & 0x04040404u;
-		if (__ballot(anyinv != 0u)) {
-			if (anyinv != 0u) {
-				// invalid flags packed like the codes: base j at bit 2j of F
-				const uint32_t Im = ((t0 >> 2) & 0x01010101u) | (t1 & 0x04040404u) |
-				                    ((t2 << 2) & 0x10101010u) | ((t3 << 4) & 0x40404040u);
-				const uint32_t F = transpose2x4x4(Im);
-				const int j0 = (int)((uint32_t)__builtin_ctz(F) >> 1);          // first invalid base
-				const int j1 = (int)((31u - (uint32_t)__builtin_clz(F)) >> 1);  // last invalid base
-				V &= ~((2u << (15 - j0)) - 1u);          // windows ending at j >= j0
-				const int u1 = 16 - j1 - K;
-				U = U < u1 ? U : u1;
-			}
-		}
-		hm &= V;
-		tl += (uint32_t)__builtin_popcount(V);
-		// queue the hit positions' forward k-mers (bit b <-> base j = 15 - b)
-		if constexpr ((ABL & 4) != 0) {
-			asm volatile("" :: "v"(hm));
-		} else if (__ballot(hm != 0u)) {
-			for (;;) {
-				const bool has = hm != 0u;
-				const uint64_t bal = __ballot(has);
-				if (!bal) break;
-				const uint32_t b = has ? 31u - (uint32_t)__builtin_clz(hm) : 0u;
-				const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, 2u * b);
-				const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
-				queue_append(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
-				hm &= ~(1u << b);
-			}
-		}
-		Bm2 = Bm1; Bm1 = Bc;
-		Cm2 = Cm1; Cm1 = Cc;
-		w0 = w4; w1 = x1; w2 = x2; w3 = x3; w4 = x4;
-		x1 = y1; x2 = y2; x3 = y3; x4 = y4;
-		wi += 4;
+		quad_fix(d1, w1, w2, w3, w4);
+		quad_fix(d5, w5, w6, w7, w8);
+		packed_chunk<K, ABL>(A, c, tail_c, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
+		packed_chunk<K, ABL>(A, c + 1, tail_c, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
+		w0 = w8;
+		w1 = n0; w2 = n1; w3 = n2; w4 = n3; d1 = dn0;
+		w5 = n4; w6 = n5; w7 = n6; w8 = n7; d5 = dn4;
+		wi += 8;
+	}
+	if (it < nit) {
+		const int c = c_lo + it;
+		quad_fix(d1, w1, w2, w3, w4);
+		quad_fix(d5, w5, w6, w7, w8);
+		packed_chunk<K, ABL>(A, c, tail_c, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
+		if (it + 1 < nit)
+			packed_chunk<K, ABL>(A, c + 1, tail_c, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl,
+			                     lane);
 	}
 }
 
@@ -579,25 +645,34 @@ vc_count_reads_kernel(VcKernelArgs A)
 	const uint64_t wmax = A.seq_words ? A.seq_words - 1 : 0;
 	unsigned long long tally = 0;
 
-	for (uint64_t g = blockIdx.x; g * (uint64_t)VC_BLOCK < A.n_reads; g += gridDim.x) {
-		const uint64_t r = g * (uint64_t)VC_BLOCK + threadIdx.x;
-		int len = 0;
-		uint64_t off = 0;
-		if (r < A.n_reads) {
-			len = (int)A.lens[r];
-			off = A.offs[r] + A.off_adj;
-			if ((uint32_t)len > VC_LONG_READ) {
-				uint32_t slot = atomicAdd(A.nlong, 1u);
-				if (slot < A.long_cap) A.longlist[slot] = (uint32_t)r;
-				len = 0;
-			}
+	// The lengths and offsets of the next read group are requested before
+	// this group is scanned (one load each, index clamped, so the compiler's
+	// count of loads in flight stays exact) and used after its queue drain.
+	const uint64_t rlast = A.n_reads - 1;
+	uint64_t g = blockIdx.x;
+	uint64_t r = g * (uint64_t)VC_BLOCK + threadIdx.x;
+	uint32_t len_raw = A.lens[r < rlast ? r : rlast];
+	uint64_t off_raw = A.offs[r < rlast ? r : rlast];
+	while (g * (uint64_t)VC_BLOCK < A.n_reads) {
+		int len = r < A.n_reads ? (int)len_raw : 0;
+		const uint64_t off = off_raw + A.off_adj;
+		if ((uint32_t)len > VC_LONG_READ) {
+			const uint32_t slot = atomicAdd(A.nlong, 1u);
+			if (slot < A.long_cap) A.longlist[slot] = (uint32_t)r;
+			len = 0;
 		}
+		const uint64_t gn = g + gridDim.x;
+		const uint64_t rn = gn * (uint64_t)VC_BLOCK + threadIdx.x;
+		len_raw = A.lens[rn < rlast ? rn : rlast];
+		off_raw = A.offs[rn < rlast ? rn : rlast];
 		const int nch = (len + 15) >> 4;
 		const int nit = wave_max_i32(nch);
 		uint32_t tl = 0;
 		scan_any<K, false, ABL>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tl, lane);
 		tally += tl;
 		queue_flush(A, Q, lane);     // one drain per read group, probes overlapped
+		g = gn;
+		r = rn;
 	}
 	queue_flush(A, Q, lane);
 	const unsigned long long t = wave_sum_u64(tally);

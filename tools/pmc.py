@@ -24,15 +24,28 @@ PASSES = [
     "TA_BUSY_avr TA_TA_BUSY_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum",
     "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum",
 ]
+# diagnosis passes (python tools/pmc.py OUTDIR --set diag [bench args...])
+DIAG = [
+    "SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_IFETCH SQ_WAIT_ANY",
+    "TCP_UTCL1_TRANSLATION_MISS TCP_UTCL1_TRANSLATION_HIT TCP_PENDING_STALL_CYCLES TCP_TCC_READ_REQ_LATENCY",
+    "SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL",
+    "SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM",
+    "TA_ADDR_STALLED_BY_TC_CYCLES TA_DATA_STALLED_BY_TC_CYCLES TCP_TCR_TCP_STALL_CYCLES TCP_READ_TAGCONFLICT_STALL_CYCLES",
+    "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU",
+]
 KERNEL = "vc_count_reads_kernel"
 
 
 def main():
     out = os.path.abspath(sys.argv[1])
-    bench_args = sys.argv[2:] or ["--steps", "2", "--warmup", "1", "--no-cpu"]
+    rest = sys.argv[2:]
+    passes = PASSES
+    if rest[:2] == ["--set", "diag"]:
+        passes, rest = DIAG, rest[2:]
+    bench_args = rest or ["--steps", "2", "--warmup", "1", "--no-cpu"]
     os.makedirs(out, exist_ok=True)
     acc = {}
-    for i, group in enumerate(PASSES):
+    for i, group in enumerate(passes):
         d = os.path.join(out, "pass%d" % i)
         cmd = ["rocprofv3", "--kernel-trace", "--pmc"] + group.split() + [
             "-d", d, "-o", "p", "--output-format", "csv", "--",
