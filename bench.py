@@ -73,19 +73,33 @@ def main():
     ap.add_argument("--k", type=int, default=21)
     ap.add_argument("--f-snp", type=float, default=0.01)
     ap.add_argument("--panel", default="grch38", choices=["grch38", "syn200k"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5"],
+                    help="BASELINE.json configs: c2 (default, the headline: k=21, 100M reads), "
+                         "c3 (k=31, 100M pairs = 200M reads of 150 bp), c5 (200k-SNP synthetic panel)")
     ap.add_argument("--cpu-reads", type=int, default=2_000_000, help="CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
+    if args.config == "c3":
+        args.k, args.reads = 31, 2 * args.reads
+    elif args.config == "c5":
+        args.panel = "syn200k"
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    # one GPU per rank; the modulo only matters for rehearsals with more ranks
+    # than GPUs (VAFC_DIST_BACKEND=gloo), never for the driver's N-GPU runs
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("VAFC_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     import vafc
     import vafc_synth as S
 
@@ -166,7 +180,9 @@ def main():
         try:
             with open(pmc) as f:
                 pj = json.load(f)
-            if pj.get("reads") == R and pj.get("read_len") == L and pj.get("k") == args.k:
+            base_reads = R // 2 if args.config == "c3" else R     # pmc.py records the --reads argument
+            if (pj.get("config", "c2") == args.config and pj.get("reads") == base_reads
+                    and pj.get("read_len") == L and pj.get("k") == args.k):
                 traffic = pj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -213,7 +229,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "Mbases/sec (+ k-mers/sec) on 150 bp FASTQ, k=21",
+            "metric": "Mbases/sec (+ k-mers/sec) on %d bp FASTQ, k=%d" % (L, args.k),
             "value": round(value, 1),
             "unit": "Mbases/sec",
             "n_gpus": world,
@@ -226,8 +242,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic (counter-based generator, seed 42; patterns from SNP_GRCh38_hg38_wChr.bed, flanks seed 12345), resident in HBM",
             "config": {
-                "workload": "C2: %dM x %d bp reads per GPU, k=%d, %s panel (%d patterns, %d keys), f_snp=%g"
-                            % (R // 1_000_000, L, args.k, args.panel, n_pat, tinfo["n_keys"], args.f_snp),
+                "workload": "%s: %dM x %d bp reads per GPU, k=%d, %s panel (%d patterns, %d keys), f_snp=%g"
+                            % (args.config.upper(), R // 1_000_000, L, args.k, args.panel, n_pat, tinfo["n_keys"], args.f_snp),
                 "reads_per_gpu": R, "read_len": L, "k": args.k, "patterns": n_pat,
                 "filter_bytes": tinfo["filter_bytes"], "table_slots": tinfo["slots"],
                 "parallelism": "dp%d (reads sharded per rank, RCCL all-reduce of uint32 counts)" % world,

@@ -81,8 +81,9 @@ def main():
         json.dump({"kernel": KERNEL, "bench_args": bench_args, "counters": acc, "derived": derived}, f, indent=1)
     # the summary bench.py reads for roofline.traffic (same workload only)
     if "hbm_bytes_per_launch" in derived:
-        summ = {"kernel": KERNEL, "reads": _arg(bench_args, "--reads", 100_000_000),
-                "read_len": _arg(bench_args, "--read-len", 150), "k": _arg(bench_args, "--k", 21),
+        cfg = bench_args[bench_args.index("--config") + 1] if "--config" in bench_args else "c2"
+        summ = {"kernel": KERNEL, "config": cfg, "reads": _arg(bench_args, "--reads", 100_000_000),
+                "read_len": _arg(bench_args, "--read-len", 150), "k": 31 if cfg == "c3" else _arg(bench_args, "--k", 21),
                 "hbm_bytes_per_launch": derived["hbm_bytes_per_launch"],
                 "hbm_read_bytes_per_launch": derived.get("hbm_read_bytes_per_launch"),
                 "hbm_write_bytes_per_launch": derived.get("hbm_write_bytes_per_launch"),
