@@ -69,6 +69,23 @@ VC_HD uint32_t vc_filter_word(uint32_t flo, uint32_t rlo, uint32_t fsh, uint32_t
 }
 VC_HD uint32_t vc_filter_mask(uint32_t flo, uint32_t rlo) { return (1u << (flo & 31u)) | (1u << (rlo & 31u)); }
 
+/* Second-level filter for large key sets (> 2^16 keys, where the LDS
+ * prefilter saturates): 2^l2bits 32-bit words in HBM, small enough to stay
+ * L2/MALL-resident, three bits per key.  The queue drain checks it before
+ * probing the exact table, whose random 16-byte slots would otherwise come
+ * from HBM for every LDS false positive.  Word from vc_hash's top bits, bits
+ * from an independent second hash of the canonical key. */
+#define VC_L2F_MIN_KEYS 65536u
+#define VC_L2F_MAX_BITS 19          /* 2 MiB */
+VC_HD uint32_t vc_hash2(uint64_t key)
+{
+	return ((uint32_t)(key >> 17) ^ (uint32_t)key) * 0x9E3779B1u;
+}
+VC_HD uint32_t vc_l2f_mask(uint32_t h2)
+{
+	return (1u << (h2 & 31u)) | (1u << ((h2 >> 5) & 31u)) | (1u << ((h2 >> 10) & 31u));
+}
+
 /* Device key table slot: 16 bytes, one load per probe step. */
 typedef struct {
 	uint64_t key;

@@ -234,6 +234,8 @@ struct vc_ctx {
 	uint32_t tbits = 0;
 	uint32_t *d_filter = nullptr;
 	uint32_t wbits = 0;
+	uint32_t *d_l2f = nullptr;             // second-level filter (large key sets only)
+	uint32_t l2bits = 0;
 	uint32_t fsh = 0;
 	uint32_t *d_counts = nullptr;          // active outputs (own or bound)
 	unsigned long long *d_tally = nullptr;
@@ -292,6 +294,13 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	while (wbits < VC_MAX_FILTER_WBITS && ((uint64_t)32 << wbits) < 24 * (uint64_t)n_keys) ++wbits;
 	const uint32_t fsh = vc_filter_shift(k, wbits);
 	std::vector<uint32_t> fw((size_t)1 << wbits, 0);
+	// second level: >= 40 bits per key, up to 2 MiB, when the LDS filter saturates
+	uint32_t l2bits = 0;
+	if (n_keys > VC_L2F_MIN_KEYS) {
+		l2bits = 12;
+		while (l2bits < VC_L2F_MAX_BITS && ((uint64_t)32 << l2bits) < 40 * (uint64_t)n_keys) ++l2bits;
+	}
+	std::vector<uint32_t> l2w(l2bits ? (size_t)1 << l2bits : 0, 0);
 	uint64_t inserted = 0;
 	for (size_t i = 0; i < n_keys; ++i) {
 		const uint64_t key = keys[i];
@@ -308,11 +317,13 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 		tab[s].val = vals[i];
 		const uint32_t flo = (uint32_t)key, rlo = (uint32_t)vc_revcomp(key, k);
 		fw[vc_filter_word(flo, rlo, fsh, wbits)] |= vc_filter_mask(flo, rlo);
+		if (l2bits) l2w[vc_hash(key) >> (32 - l2bits)] |= vc_l2f_mask(vc_hash2(key));
 		++inserted;
 	}
 	c->n_keys = inserted;
 	c->tbits = tbits;
 	c->wbits = wbits;
+	c->l2bits = l2bits;
 	c->fsh = fsh;
 	c->ablate = getenv("VAFC_ABLATE") ? atoi(getenv("VAFC_ABLATE")) : 0;
 
@@ -338,6 +349,10 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	TRY(hipMemset(c->d_pad, 0, 64));
 	TRY(hipMemcpy(c->d_table, tab.data(), tslots * sizeof(vc_slot_t), hipMemcpyHostToDevice));
 	TRY(hipMemcpy(c->d_filter, fw.data(), fw.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+	if (l2bits) {
+		TRY(hipMalloc(&c->d_l2f, l2w.size() * sizeof(uint32_t)));
+		TRY(hipMemcpy(c->d_l2f, l2w.data(), l2w.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+	}
 	TRY(hipMemset(c->d_counts, 0, (2 * (size_t)n_patterns + 2) * sizeof(uint32_t)));
 	TRY(hipMemset(c->d_tally, 0, sizeof(unsigned long long)));
 	TRY(hipEventCreate(&c->t0));
@@ -383,6 +398,7 @@ extern "C" void vc_destroy(vc_ctx *c)
 	if (c->t1) (void)hipEventDestroy(c->t1);
 	if (c->d_table) (void)hipFree(c->d_table);
 	if (c->d_filter) (void)hipFree(c->d_filter);
+	if (c->d_l2f) (void)hipFree(c->d_l2f);
 	if (c->own_counts) (void)hipFree(c->own_counts);
 	if (c->own_tally) (void)hipFree(c->own_tally);
 	if (c->d_nlong) (void)hipFree(c->d_nlong);
@@ -420,6 +436,8 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 	A.filter = c->d_filter;
 	A.wbits = c->wbits;
 	A.fsh = c->fsh;
+	A.l2f = c->d_l2f;
+	A.l2bits = c->l2bits;
 	A.ablate = c->ablate;
 	A.k = c->k;
 	A.kmask = ((uint64_t)1 << (2 * c->k)) - 1;

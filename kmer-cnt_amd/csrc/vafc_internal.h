@@ -25,6 +25,8 @@ struct VcKernelArgs {
 	const uint32_t *filter;      // 2^wbits 32-bit words
 	uint32_t wbits;
 	uint32_t fsh;                // filter word shift (vc_filter_shift)
+	const uint32_t *l2f;         // second-level filter (vc_l2f_*), NULL = off
+	uint32_t l2bits;
 	int ablate;                  // ablation builds only (VAFC_ABLATE), 0 otherwise
 	int k;
 	uint64_t kmask;              // (1 << 2k) - 1

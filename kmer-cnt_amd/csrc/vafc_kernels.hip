@@ -162,10 +162,55 @@ struct WaveQueue {
 // Probe the exact table for queue entries [lo, hi) (up to 4 per lane); the
 // first table load of every entry is issued before any is resolved, so one
 // memory latency covers the whole drain.
+// Large key sets: every entry is first checked against the second-level
+// filter (one L2-resident dword), and only survivors probe the exact table.
+__device__ __forceinline__ void drain_range_l2f(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
+                                             uint32_t hi, int lane)
+{
+	uint64_t key[4];
+	uint32_t h[4], w[4], m[4];
+	const uint32_t l2sh = 32u - A.l2bits;
+#pragma unroll
+	for (int r = 0; r < 4; ++r) {
+		const uint32_t i = lo + (uint32_t)(r * WAVE + lane);
+		key[r] = VC_EMPTY_KEY;
+		h[r] = 0;
+		w[r] = 0;
+		m[r] = 1;
+		if (i < hi) {
+			const uint64_t f = q[i] & A.kmask;
+			const uint64_t rc = revcomp_dev(f, A.k);
+			key[r] = f < rc ? f : rc;
+			h[r] = vc_hash(key[r]);
+			m[r] = vc_l2f_mask(vc_hash2(key[r]));
+			w[r] = A.l2f[h[r] >> l2sh];
+		}
+	}
+#pragma unroll
+	for (int r = 0; r < 4; ++r) {
+		if ((w[r] & m[r]) != m[r]) continue;      // also skips empty entries (w = 0, m = 1)
+		uint32_t t = vc_table_slot(h[r], A.tbits);
+		for (;;) {
+			const uint4 e = *reinterpret_cast<const uint4 *>(&A.table[t]);
+			const uint64_t k2 = ((uint64_t)e.y << 32) | e.x;
+			if (k2 == key[r]) {
+				atomicAdd(&A.counts[e.z], 1u);
+				break;
+			}
+			if (k2 == VC_EMPTY_KEY) break;
+			t = (t + 1u) & A.tmask;
+		}
+	}
+}
+
 __device__ __forceinline__ void drain_range(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
                                             uint32_t hi, int lane)
 {
 	__builtin_amdgcn_wave_barrier();
+	if (A.l2bits) {
+		drain_range_l2f(A, q, lo, hi, lane);
+		return;
+	}
 	uint64_t key[4];
 	uint32_t s[4];
 	uint4 e[4];
