@@ -58,7 +58,14 @@ VC_HD uint64_t vc_revcomp(uint64_t x, int k)
  * words empty; the product's middle bits mix all 48 input bits. */
 VC_HD uint32_t vc_filter_shift(int k, uint32_t wbits)
 {
-	/* the product has 4k significant bits; skip its skewed top 4 */
+	/* SNP panels hold ref/alt k-mer pairs that differ only in the centre base
+	 * (bits k-1, k of flo and of rlo): keep it out of the word and the pair
+	 * sets the same two bits, halving the filter's load.  The product's bits
+	 * [lo, lo+wbits) depend on operand bits [0, lo+wbits) only; lo >= 5 keeps
+	 * the word independent of the bit positions (operand bits 0..4). */
+	if (k - 1 >= 24) return 32u - wbits;                     /* centre outside lo24 */
+	if (k - 1 - (int)wbits >= 5) return 5u;                  /* centre above the word */
+	/* otherwise: the top wbits of the product's 4k significant bits, skipping its skewed top 4 */
 	const int top = 4 * k - 4 < 32 ? 4 * k - 4 : 32;
 	return top > (int)wbits ? (uint32_t)(top - (int)wbits) : 0u;
 }

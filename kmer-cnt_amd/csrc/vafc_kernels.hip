@@ -480,6 +480,7 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 {
 	constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
 	const uint32_t fsh = A.fsh;
+	const uint32_t wmask4 = ((1u << A.wbits) - 1u) << 2;
 	const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
 	const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
 	const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
@@ -506,9 +507,10 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 		uint32_t rlo;
 		if (s2 >= 16) rlo = __builtin_amdgcn_alignbit(Cc, Cm1, (uint32_t)(2 * (s2 - 16)));
 		else rlo = __builtin_amdgcn_alignbit(Cm1, Cm2, (uint32_t)(2 * s2));
-		const uint32_t widx = vc_filter_mix(flo, rlo) >> fsh;   // < 2^wbits: fsh = 32 - wbits for k >= 9
-		if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); fw[j] = widx; }
-		else fw[j] = filt[widx];
+		// byte address of word (mix >> fsh) & (2^wbits - 1): fsh >= 5 for k >= 17
+		const uint32_t wba = (vc_filter_mix(flo, rlo) >> (fsh - 2u)) & wmask4;
+		if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(wba)); fw[j] = wba; }
+		else fw[j] = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(filt) + wba);
 		fm[j] = vc_filter_mask(flo, rlo);
 	}
 #pragma unroll
@@ -613,6 +615,7 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	int U = 1 - K - vlo + 16 * c_lo;                 // +16 at the top of every chunk
 	int Qe = -vhi + 16 * c_lo;
 
+	[[maybe_unused]] uint32_t abl_sink = 0;
 	int it = 0;
 	for (; it + 2 < nit; it += 2) {
 		const int c = c_lo + it;
@@ -621,6 +624,23 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 			n0 = (uint32_t)wi * 0x9E3779B1u; n1 = n0 ^ 0x41434754u; n2 = n0 + 0x54474341u; n3 = n0 * 5u;
 			n4 = n0 ^ 0x5A5A5A5Au; n5 = n1 + 7u; n6 = n2 ^ n3; n7 = n4 * 3u;
 			dn0 = dn4 = 0;
+		} else if constexpr ((ABL & 16) != 0) {
+			// timing experiment: issue the real loads but consume them only
+			// after the scan (isolates the cost of waiting from issuing)
+			uint32_t t0_, t1_, t2_, t3_, t4_, t5_, t6_, t7_;
+			ldq(s32, wi + 9, wmax, t0_, t1_, t2_, t3_);
+			ldq(s32, wi + 13, wmax, t4_, t5_, t6_, t7_);
+			abl_sink ^= t0_ ^ t1_ ^ t2_ ^ t3_ ^ t4_ ^ t5_ ^ t6_ ^ t7_;
+			n0 = (uint32_t)wi * 0x9E3779B1u; n1 = n0 ^ 0x41434754u; n2 = n0 + 0x54474341u; n3 = n0 * 5u;
+			n4 = n0 ^ 0x5A5A5A5Au; n5 = n1 + 7u; n6 = n2 ^ n3; n7 = n4 * 3u;
+			dn0 = dn4 = 0;
+		} else if constexpr ((ABL & 8) != 0) {
+			// timing experiment: the memory pattern of a wave-tiled layout
+			// (chunk c of lane l at 16 * (64 c + l) from a wave base)
+			const uint64_t tb = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(off >> 4)) << 2) +
+			                    (uint64_t)(64 * (it + 2) + lane) * 4u;
+			dn0 = ldq(s32, tb, wmax, n0, n1, n2, n3);
+			dn4 = ldq(s32, tb + 256, wmax, n4, n5, n6, n7);
 		} else {
 			dn0 = ldq(s32, wi + 9, wmax, n0, n1, n2, n3);
 			dn4 = ldq(s32, wi + 13, wmax, n4, n5, n6, n7);
@@ -634,6 +654,7 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 		w5 = n4; w6 = n5; w7 = n6; w8 = n7; d5 = dn4;
 		wi += 8;
 	}
+	if constexpr ((ABL & 16) != 0) tl += abl_sink & 1u;
 	if (it < nit) {
 		const int c = c_lo + it;
 		quad_fix(d1, w1, w2, w3, w4);
@@ -881,7 +902,7 @@ static hipError_t launch_kw(const VcKernelArgs *A, int grid, int grid_long, hipS
 }
 
 #ifdef VC_ABLATION
-#define VC_ABL_LIST(X) X(1) X(2) X(4) X(3) X(5) X(6) X(7)
+#define VC_ABL_LIST(X) X(1) X(2) X(4) X(3) X(5) X(6) X(7) X(8) X(12) X(16) X(20)
 #endif
 
 template <int K>

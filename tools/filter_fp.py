@@ -3,8 +3,9 @@
 
 Builds the filter exactly as vc_create does (vafc_common.h) for the GRCh38
 panel's k=21 keys and queries 2M uniform random 21-mers.  Also evaluates the
-earlier sum-based word index, whose bits at the centre base of an odd k are
-constant (fwd and revcomp add to 3 there), to document why the product is used.
+earlier word indices: the sum of the strands (constant at the centre base of
+an odd k: fwd and revcomp add to 3 there) and the product's top bits (which
+separate a SNP's ref and alt k-mers, doubling the filter load).
     python tools/filter_fp.py
 """
 import os
@@ -32,10 +33,10 @@ def lo(x):
     return (x & M32).astype(np.uint32)
 
 
-def product_filter(ks):       # vafc_common.h: vc_filter_word / vc_filter_mask
+def product_filter(ks, lo_bit=5):   # vafc_common.h: vc_filter_word / vc_filter_mask (k=21: lo 5)
     fl, rl = lo(ks), lo(revcomp(ks))
     pr = ((fl.astype(np.uint64) & M24) * (rl.astype(np.uint64) & M24)) & M32
-    w = (pr >> np.uint64(32 - WBITS)).astype(np.uint32)
+    w = ((pr >> np.uint64(lo_bit)) & np.uint64((1 << WBITS) - 1)).astype(np.uint32)
     m = (np.uint32(1) << (fl & np.uint32(31))) | (np.uint32(1) << (rl & np.uint32(31)))
     return w, m
 
@@ -57,13 +58,15 @@ def main():
     keys, _, _ = vafc.load_patterns(pat).keys(K)
     keys = np.unique(np.asarray(keys, dtype=np.uint64))
     q = np.random.default_rng(1).integers(0, 1 << (2 * K), size=2_000_000, dtype=np.uint64)
-    for name, fn in (("product (current)", product_filter), ("sum (v6)", sum_filter)):
+    for name, fn in (("product, bits 5..19 (current: centre base excluded)", product_filter),
+                     ("product, bits 17..31 (v7)", lambda ks: product_filter(ks, 32 - WBITS)),
+                     ("sum (v6)", sum_filter)):
         F = np.zeros(1 << WBITS, dtype=np.uint32)
         w, m = fn(keys)
         np.bitwise_or.at(F, w, m)
         qw, qm = fn(q)
         fp = float(np.mean((F[qw] & qm) == qm))
-        print("%-18s keys %d  words used %5d / %d  FP %.4f" % (name, len(keys), np.count_nonzero(F), 1 << WBITS, fp))
+        print("%-52s keys %d  words used %5d / %d  FP %.4f" % (name, len(keys), np.count_nonzero(F), 1 << WBITS, fp))
 
 
 if __name__ == "__main__":
