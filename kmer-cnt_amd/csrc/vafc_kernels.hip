@@ -122,6 +122,19 @@ __device__ __forceinline__ void ld4(const uint32_t *__restrict__ s32, uint64_t i
 	}
 }
 
+// LDS word at byte offset (x & m) from an LDS base whose low bits are clear:
+// one v_and_or_b32 forms the address (base | offset), which the compiler
+// would otherwise add with a separate v_add (the base is a link-time symbol).
+typedef const uint32_t __attribute__((address_space(3))) lds_u32_t;
+__device__ __forceinline__ uint32_t lds_base(const uint32_t *p)
+{
+	return (uint32_t)(uintptr_t)(lds_u32_t *)p;
+}
+__device__ __forceinline__ uint32_t lds_word(uint32_t base, uint32_t x, uint32_t m)
+{
+	return *(lds_u32_t *)(uintptr_t)((x & m) | base);
+}
+
 // ---------------------------------------------------------------------------
 // exact table probe (drain side)
 // ---------------------------------------------------------------------------
@@ -481,6 +494,7 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 	constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
 	const uint32_t fsh = A.fsh;
 	const uint32_t wmask4 = ((1u << A.wbits) - 1u) << 2;
+	const uint32_t fbase = lds_base(filt);       // the filter sits at a 16-byte aligned LDS base
 	const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
 	const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
 	const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
@@ -499,7 +513,9 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 	const uint32_t Bc = pairrev(L);                  // big-endian codes
 
 	uint32_t hm = 0;                                 // filter pass, bit 15 - j for base j
-	uint32_t fw[16], fm[16];
+	// pass <=> bits (flo & 31) and (rlo & 31) of the filter word are set:
+	// hm = (hm << 1) | ((w >> flo) & (w >> rlo) & 1), 4 VALU per window
+	uint32_t fw[16], fl[16], rl[16];
 #pragma unroll
 	for (int j = 0; j < 16; ++j) {
 		const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, (uint32_t)(2 * (15 - j)));
@@ -508,19 +524,15 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 		if (s2 >= 16) rlo = __builtin_amdgcn_alignbit(Cc, Cm1, (uint32_t)(2 * (s2 - 16)));
 		else rlo = __builtin_amdgcn_alignbit(Cm1, Cm2, (uint32_t)(2 * s2));
 		// byte address of word (mix >> fsh) & (2^wbits - 1): fsh >= 5 for k >= 17
-		const uint32_t wba = (vc_filter_mix(flo, rlo) >> (fsh - 2u)) & wmask4;
-		if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(wba)); fw[j] = wba; }
-		else fw[j] = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(filt) + wba);
-		fm[j] = vc_filter_mask(flo, rlo);
+		const uint32_t wsh = vc_filter_mix(flo, rlo) >> (fsh - 2u);
+		if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(wsh)); fw[j] = wsh; }
+		else fw[j] = lds_word(fbase, wsh, wmask4);
+		fl[j] = flo;
+		rl[j] = rlo;
 	}
 #pragma unroll
-	for (int j = 0; j < 16; ++j) {
-		// hm = 2*hm + pass with the pass wave mask as carry-in: one v_addc
-		const uint64_t pb = __ballot((~fw[j] & fm[j]) == 0u);
-		uint64_t cout;
-		asm volatile("v_addc_co_u32 %0, %1, %2, %2, %3" : "=v"(hm), "=s"(cout) : "v"(hm), "s"(pb));
-		(void)cout;
-	}
+	for (int j = 0; j < 16; ++j)
+		hm = (hm << 1) | ((fw[j] >> (fl[j] & 31u)) & (fw[j] >> (rl[j] & 31u)) & 1u);
 	// windows of this chunk inside [vlo, vhi) with no earlier invalid base
 	uint32_t V = ((1u << clamp16(U)) - 1u) & ~((1u << clamp16(Qe)) - 1u);
 	const uint32_t anyinv = (t0 | t1 | t2 | t3) & 0x04040404u;
