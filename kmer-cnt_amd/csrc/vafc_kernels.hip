@@ -559,11 +559,12 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 			const bool has = hm != 0u;
 			const uint64_t bal = __ballot(has);
 			if (!bal) break;
-			const uint32_t b = has ? 31u - (uint32_t)__builtin_clz(hm) : 0u;
+			// lowest pass first; lanes without one compute a garbage key they do not append
+			const uint32_t b = (uint32_t)__builtin_ctz(hm | 0x80000000u);   // hm < 2^16
 			const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, 2u * b);
 			const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
 			queue_append(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
-			hm &= ~(1u << b);
+			hm &= hm - 1u;
 		}
 	}
 	Bm2 = Bm1; Bm1 = Bc;
