@@ -1,815 +1,16 @@
-// vafc_kernels.hip -- HIP kernels of the vaf-counter hot path for gfx950 (CDNA4).
-//
-// Replaces steps 1+2 of the reference pipeline: the SSSE3 2-bit encode
-// (vaf-counter.c:261-291), the rolling canonical k-mer extraction
-// (vaf-counter.c:349-427) and the khashl lookup + relaxed atomic increment
-// (vaf-counter.c:449-479, khashl.h:137-150).  Integer work only, no MFMA.
-//
-// Design (DESIGN.md has the full story):
-//  * One lane per read, one wave = 64 reads, 1024-thread persistent blocks
-//    (one per CU, 16 waves/CU) grid-striding over groups of 1024 reads.
-//  * Read bytes are fetched as dwords from the read's 4-byte-aligned start and
-//    realigned with v_alignbyte; 16 bases (one "chunk") per loop trip, with
-//    the next chunk's dwords in flight during the current one.
-//  * Decode is SWAR on 4 bytes at a time with v_perm_b32 as a 8-entry LUT --
-//    the same nibble table as the reference's PSHUFB; the reference decodes
-//    the last len%16 bytes of a read with seq_nt4_table instead, so the lane
-//    switches to an exact SWAR seq_nt4_table for that tail chunk.
-//  * Rolling forward / reverse-complement k-mers in 64-bit registers; validity
-//    from a 32-bit shift register of invalid-base flags (a window is valid iff
-//    its last k flags are zero) -- equivalent to the reference's reset-on-N.
-//  * Every valid canonical k-mer probes a blocked Bloom filter held in LDS
-//    (2 bits in one 32-bit word, up to 128 KiB).  Filter hits are compacted
-//    per wave into an LDS queue (ballot + mbcnt); a full queue is drained by
-//    all 64 lanes probing the exact HBM/L2-resident table at once, and hits do
-//    atomicAdd on uint32 counts[(pattern<<1)|is_alt].
-//  * Reads longer than VC_LONG_READ are appended to a list and counted by a
-//    second kernel in which every lane of the grid takes a VC_LONG_SEG-base
-//    segment (plus a k-1 halo) of the read.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-#include "vafc_common.h"
-#include "vafc_internal.h"
+// vafc_kernels.hip -- dispatch of the counting kernels on k (the K = 16..31
+// instantiations live in vafc_kernels_kNN.hip, k < 16 runs the run-time-k
+// kernel instantiated here), plus the decode test hook and the synthetic
+// read generator.
+#include "vafc_scan.h"
 
-#define WAVE 64
-
-// ---------------------------------------------------------------------------
-// small helpers
-// ---------------------------------------------------------------------------
-
-// Wave maximum of a small non-negative value (< 2048) from 11 ballots: no
-// cross-lane data movement, so no LDS round trips.
-__device__ __forceinline__ int wave_max_i32(int v)
-{
-	int m = 0;
-#pragma unroll
-	for (int b = 10; b >= 0; --b) {
-		const int t = m | (1 << b);
-		if (__ballot(v >= t)) m = t;
-	}
-	return m;
-}
-
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
-{
-#pragma unroll
-	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
-	return v;
-}
-
-// Nibble LUT of the reference's PSHUFB decode (vaf-counter.c:272-275) for
-// low nibbles 0..7, {4,0,4,1,3,3,4,2}; nibbles 8..15 are all 4 (invalid).
-// v_perm_b32 selector bytes 0..3 pick bytes of the 2nd operand, 4..7 of the 1st.
-#define NIB_LO 0x01040004u
-#define NIB_HI 0x02040303u
-// Expected high nibble (with the lower-case bit cleared) of an ACGTU letter
-// for each low nibble 0..7; 0xFF never matches.
-#define LET_LO 0x04FF04FFu
-#define LET_HI 0x04FF0505u
-
-// Head decode of 4 bytes: code byte = LUT[b & 15]; bit 2 set <=> invalid.
-__device__ __forceinline__ uint32_t dec_head(uint32_t b)
-{
-	uint32_t t = __builtin_amdgcn_perm(NIB_HI, NIB_LO, b & 0x07070707u);
-	return t | ((b >> 1) & 0x04040404u);
-}
-
-// Tail decode = seq_nt4_table (vaf-counter.c:73-90) on 4 bytes: ACGTU/acgtu
-// keep their nibble code, bytes 0..3 map to themselves, all else invalid.
-__device__ __forceinline__ uint32_t dec_tail(uint32_t b)
-{
-	uint32_t t = dec_head(b);
-	uint32_t e = __builtin_amdgcn_perm(LET_HI, LET_LO, b & 0x07070707u);
-	uint32_t m = ((b >> 4) & 0x0D0D0D0Du) ^ e;
-	uint32_t nz = (((m & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | m) & 0x80808080u;  // byte != 0
-	t |= nz >> 5;
-	uint32_t y = b & 0xFCFCFCFCu;
-	uint32_t small = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u; // byte < 4
-	uint32_t sel = (small >> 7) * 0xFFu;
-	return (t & ~sel) | (b & sel);
-}
-
-// Invalid-flag mask for the bytes of a word whose first position is P, given
-// the valid position range [lo, hi): bytes outside get bit 2 set.
-__device__ __forceinline__ uint32_t range_mask_hi(int rel_hi)
-{
-	// bytes i >= rel_hi are outside
-	return rel_hi >= 4 ? 0u : (rel_hi <= 0 ? 0x04040404u : (0x04040404u << (8 * rel_hi)));
-}
-__device__ __forceinline__ uint32_t range_mask_lo(int rel_lo)
-{
-	// bytes i < rel_lo are outside
-	return rel_lo <= 0 ? 0u : (rel_lo >= 4 ? 0x04040404u : (0x04040404u & ((1u << (8 * rel_lo)) - 1u)));
-}
-
-__device__ __forceinline__ uint32_t ldw(const uint32_t *__restrict__ s32, uint64_t i, uint64_t wmax)
-{
-	return s32[i < wmax ? i : wmax];
-}
-
-// Four consecutive dwords from a 4-byte-aligned index: one global_load_dwordx4
-// when all four are inside the buffer, else four clamped dword loads (the
-// last reads of a batch).  Loaded bytes past a read's end are masked later.
-typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-__device__ __forceinline__ void ld4(const uint32_t *__restrict__ s32, uint64_t i, uint64_t wmax,
-                                    uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
-{
-	if (i + 3 <= wmax) {
-		const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(s32 + i);
-		a = v.x; b = v.y; c = v.z; d = v.w;
-	} else {
-		a = ldw(s32, i, wmax); b = ldw(s32, i + 1, wmax); c = ldw(s32, i + 2, wmax); d = ldw(s32, i + 3, wmax);
-	}
-}
-
-// LDS word at byte offset (x & m) from an LDS base whose low bits are clear:
-// one v_and_or_b32 forms the address (base | offset), which the compiler
-// would otherwise add with a separate v_add (the base is a link-time symbol).
-typedef const uint32_t __attribute__((address_space(3))) lds_u32_t;
-__device__ __forceinline__ uint32_t lds_base(const uint32_t *p)
-{
-	return (uint32_t)(uintptr_t)(lds_u32_t *)p;
-}
-__device__ __forceinline__ uint32_t lds_word(uint32_t base, uint32_t x, uint32_t m)
-{
-	return *(lds_u32_t *)(uintptr_t)((x & m) | base);
-}
-
-// ---------------------------------------------------------------------------
-// exact table probe (drain side)
-// ---------------------------------------------------------------------------
-
-// Reverse complement of a right-aligned k-mer with bit tricks (drain side only).
-__device__ __forceinline__ uint64_t revcomp_dev(uint64_t x, int k)
-{
-	const uint32_t lo = __builtin_bitreverse32((uint32_t)x), hi = __builtin_bitreverse32((uint32_t)(x >> 32));
-	uint64_t r = ((uint64_t)lo << 32) | hi;                                  // bit-reversed
-	r = ((r >> 1) & 0x5555555555555555ull) | ((r & 0x5555555555555555ull) << 1); // restore 2-bit order
-	return (~r) >> (64 - 2 * k);
-}
-
-// key: the raw forward k-mer (bits above 2k may hold older bases).
-__device__ __forceinline__ void probe_and_count(const VcKernelArgs &A, uint64_t fwd_raw)
-{
-	const uint64_t f = fwd_raw & A.kmask;
-	const uint64_t r = revcomp_dev(f, A.k);
-	const uint64_t key = f < r ? f : r;
-	uint32_t s = vc_table_slot(vc_hash(key), A.tbits);
-	for (;;) {
-		const uint4 e = *reinterpret_cast<const uint4 *>(&A.table[s]);
-		const uint64_t k2 = ((uint64_t)e.y << 32) | e.x;
-		if (k2 == key) {
-			atomicAdd(&A.counts[e.z], 1u);
-			break;
-		}
-		if (k2 == VC_EMPTY_KEY) break;
-		s = (s + 1u) & A.tmask;
-	}
-}
-
-struct WaveQueue {
-	uint64_t *q;     // LDS, VC_QCAP entries
-	uint32_t n;      // wave-uniform fill
-};
-
-// Probe the exact table for queue entries [lo, hi) (up to 4 per lane); the
-// first table load of every entry is issued before any is resolved, so one
-// memory latency covers the whole drain.
-// Large key sets: every entry is first checked against the second-level
-// filter (one L2-resident dword), and only survivors probe the exact table.
-__device__ __forceinline__ void drain_range_l2f(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
-                                             uint32_t hi, int lane)
-{
-	uint64_t key[4];
-	uint32_t h[4], w[4], m[4];
-	const uint32_t l2sh = 32u - A.l2bits;
-#pragma unroll
-	for (int r = 0; r < 4; ++r) {
-		const uint32_t i = lo + (uint32_t)(r * WAVE + lane);
-		key[r] = VC_EMPTY_KEY;
-		h[r] = 0;
-		w[r] = 0;
-		m[r] = 1;
-		if (i < hi) {
-			const uint64_t f = q[i] & A.kmask;
-			const uint64_t rc = revcomp_dev(f, A.k);
-			key[r] = f < rc ? f : rc;
-			h[r] = vc_hash(key[r]);
-			m[r] = vc_l2f_mask(vc_hash2(key[r]));
-			w[r] = A.l2f[h[r] >> l2sh];
-		}
-	}
-#pragma unroll
-	for (int r = 0; r < 4; ++r) {
-		if ((w[r] & m[r]) != m[r]) continue;      // also skips empty entries (w = 0, m = 1)
-		uint32_t t = vc_table_slot(h[r], A.tbits);
-		for (;;) {
-			const uint4 e = *reinterpret_cast<const uint4 *>(&A.table[t]);
-			const uint64_t k2 = ((uint64_t)e.y << 32) | e.x;
-			if (k2 == key[r]) {
-				atomicAdd(&A.counts[e.z], 1u);
-				break;
-			}
-			if (k2 == VC_EMPTY_KEY) break;
-			t = (t + 1u) & A.tmask;
-		}
-	}
-}
-
-__device__ __forceinline__ void drain_range(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
-                                            uint32_t hi, int lane)
-{
-	__builtin_amdgcn_wave_barrier();
-	if (A.l2bits) {
-		drain_range_l2f(A, q, lo, hi, lane);
-		return;
-	}
-	uint64_t key[4];
-	uint32_t s[4];
-	uint4 e[4];
-#pragma unroll
-	for (int r = 0; r < 4; ++r) {
-		const uint32_t i = lo + (uint32_t)(r * WAVE + lane);
-		key[r] = VC_EMPTY_KEY;
-		s[r] = 0;
-		if (i < hi) {
-			const uint64_t f = q[i] & A.kmask;
-			const uint64_t rc = revcomp_dev(f, A.k);
-			key[r] = f < rc ? f : rc;
-			s[r] = vc_table_slot(vc_hash(key[r]), A.tbits);
-			e[r] = *reinterpret_cast<const uint4 *>(&A.table[s[r]]);
-		}
-	}
-#pragma unroll
-	for (int r = 0; r < 4; ++r) {
-		if (key[r] == VC_EMPTY_KEY) continue;
-		uint4 x = e[r];
-		uint32_t t = s[r];
-		for (;;) {
-			const uint64_t k2 = ((uint64_t)x.y << 32) | x.x;
-			if (k2 == key[r]) {
-				atomicAdd(&A.counts[x.z], 1u);
-				break;
-			}
-			if (k2 == VC_EMPTY_KEY) break;
-			t = (t + 1u) & A.tmask;
-			x = *reinterpret_cast<const uint4 *>(&A.table[t]);
-		}
-	}
-}
-
-// Lanes with `hit` append `key` (bal = ballot(hit) != 0).  The queue is
-// normally drained once per read group (queue_flush); only a nearly full
-// queue is drained here, 64 entries from its top.
-__device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q, uint64_t bal,
-                                             bool hit, uint64_t key, int lane)
-{
-	const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-	                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-	if (hit) Q.q[Q.n + pre] = key;
-	Q.n = __builtin_amdgcn_readfirstlane(Q.n + (uint32_t)__popcll(bal));
-	if (Q.n > VC_QCAP - WAVE) {
-		drain_range(A, Q.q, Q.n - WAVE, Q.n, lane);
-		Q.n -= WAVE;
-		// leave nothing in flight on this (rare) path, so that the compiler
-		// can keep counting the scan's prefetches across it
-		__builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-	}
-}
-
-__device__ __forceinline__ void queue_flush(const VcKernelArgs &A, WaveQueue &Q, int lane)
-{
-	if (Q.n) drain_range(A, Q.q, 0, Q.n, lane);
-	Q.n = 0;
-}
-
-// ---------------------------------------------------------------------------
-// rolling forward / reverse-complement k-mers (vaf-counter.c:368-394)
-// ---------------------------------------------------------------------------
-//
-// K > 0: compile-time k, k-mers held as 32-bit halves and rolled with
-// v_alignbit / v_lshl_or; K == 0: run-time k on 64-bit values.  Instead of
-// resetting on an invalid base (the reference's `l = 0; x = 0`), a 32-bit
-// register of invalid flags is shifted right with v_alignbit (newest flag in
-// bit 31): the window is valid iff its top k bits are zero, i.e. the register
-// is below 2^(32-k).  fwd/rev hold exactly the last k codes once it is.
-template <int K>
-struct Roller {
-	uint32_t flo, fhi, rlo, rhi, inv;
-	uint32_t vthr;        // valid <=> inv < vthr
-	uint64_t kmask;
-	uint32_t rsh;
-
-	__device__ __forceinline__ void init(const VcKernelArgs &A)
-	{
-		flo = fhi = rlo = rhi = 0;
-		inv = 0xFFFFFFFFu;
-		const int k = K ? K : A.k;
-		vthr = 1u << (32 - k);
-		kmask = A.kmask;
-		rsh = 2u * (uint32_t)(k - 1);
-	}
-	// c: 2-bit code, bad: bit 0 = invalid flag (higher bits ignored)
-	__device__ __forceinline__ void push(uint32_t c, uint32_t bad)
-	{
-		const uint32_t cc = c ^ 3u;
-		if constexpr (K >= 17) {
-			constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
-			fhi = __builtin_amdgcn_alignbit(fhi, flo, 30) & HIM;
-			flo = (flo << 2) | c;
-			rlo = __builtin_amdgcn_alignbit(rhi, rlo, 2);
-			rhi = (rhi >> 2) | (cc << (2 * K - 34));
-		} else if constexpr (K > 0) {
-			constexpr uint32_t M = K == 16 ? 0xFFFFFFFFu : ((1u << (2 * K)) - 1u);
-			flo = ((flo << 2) | c) & M;
-			rlo = (rlo >> 2) | (cc << (2 * K - 2));
-		} else {
-			uint64_t f = ((((uint64_t)fhi << 32) | flo) << 2 | c) & kmask;
-			uint64_t r = ((((uint64_t)rhi << 32) | rlo) >> 2) | ((uint64_t)cc << rsh);
-			flo = (uint32_t)f; fhi = (uint32_t)(f >> 32);
-			rlo = (uint32_t)r; rhi = (uint32_t)(r >> 32);
-		}
-		inv = __builtin_amdgcn_alignbit(bad, inv, 1);
-	}
-	__device__ __forceinline__ bool valid() const { return inv < vthr; }
-};
-
-__device__ __forceinline__ uint64_t canonical_of(uint32_t flo, uint32_t fhi, uint32_t rlo, uint32_t rhi)
-{
-	const uint64_t f = ((uint64_t)fhi << 32) | flo, r = ((uint64_t)rhi << 32) | rlo;
-	return f < r ? f : r;
-}
-
-// ---------------------------------------------------------------------------
-// scan one span of one read per lane, wave-uniform trip count
-// ---------------------------------------------------------------------------
-//
-// Lane processes chunks [c_lo, c_hi) of its read (chunk c = read positions
-// 16c..16c+15), emitting the canonical k-mers whose whole window lies in the
-// valid position range [vlo, vhi) (vlo = 0, vhi = len for a whole read).
-// The lane's count of valid k-mers accumulates in `tl`.
-// ABL (ablation builds only, -DVC_ABLATION; results are wrong by design):
-//   1 = no LDS filter reads, 2 = no global read-byte loads, 4 = no queue appends
-template <int K, bool HAS_LO, int ABL = 0>
-__device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
-                                          uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
-                                          int vlo, int vhi, int nit, const uint32_t *__restrict__ filt,
-                                          WaveQueue &Q, uint32_t &tl, int lane)
-{
-	const uint32_t fsh = A.fsh;
-	const uint32_t zero_word = 1u << A.wbits;   // an all-zero LDS word past the filter
-	const int tail_c = (len & 15) ? (len >> 4) : -1;
-
-	uint64_t addr = off + 16ull * (uint64_t)c_lo;
-	uint64_t wi = addr >> 2;
-	const uint32_t sh = (uint32_t)(addr & 3u);
-	uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
-	uint32_t x1 = 0, x2 = 0, x3 = 0, x4 = 0;
-	if (c_lo < c_hi) {
-		ld4(s32, wi, wmax, w0, w1, w2, w3);
-		w4 = ldw(s32, wi + 4, wmax);
-	}
-	if (c_lo + 1 < c_hi) ld4(s32, wi + 5, wmax, x1, x2, x3, x4);
-	Roller<K> R;
-	R.init(A);
-
-	for (int it = 0; it < nit; ++it) {
-		const int c = c_lo + it;
-		// the dwords of the next two chunks are in flight while this one is processed
-		uint32_t y1 = 0, y2 = 0, y3 = 0, y4 = 0;
-		if (c + 2 < c_hi) {
-			if constexpr ((ABL & 2) != 0) {
-				y1 = (uint32_t)wi * 0x9E3779B1u; y2 = y1 ^ 0x41434754u; y3 = y1 + 0x54474341u; y4 = y1 * 5u;
-			} else {
-				ld4(s32, wi + 9, wmax, y1, y2, y3, y4);
-			}
-		}
-		const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
-		const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
-		const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
-		const uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
-		uint32_t t0 = dec_head(b0), t1 = dec_head(b1), t2 = dec_head(b2), t3 = dec_head(b3);
-		if (__ballot(c == tail_c)) {
-			if (c == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
-		}
-		const int P = 16 * c;
-		if (__ballot(P + 16 > vhi)) {   // past the span end (and inactive lanes: P >= vhi)
-			t0 |= range_mask_hi(vhi - P);
-			t1 |= range_mask_hi(vhi - P - 4);
-			t2 |= range_mask_hi(vhi - P - 8);
-			t3 |= range_mask_hi(vhi - P - 12);
-		}
-		if (HAS_LO) {
-			if (__ballot(P < vlo)) {
-				t0 |= range_mask_lo(vlo - P);
-				t1 |= range_mask_lo(vlo - P - 4);
-				t2 |= range_mask_lo(vlo - P - 8);
-				t3 |= range_mask_lo(vlo - P - 12);
-			}
-		}
-
-#pragma unroll
-		for (int half = 0; half < 2; ++half) {
-			const uint32_t ta = half ? t2 : t0, tb = half ? t3 : t1;
-			uint32_t fl[8], fh[8], fw[8], fm[8];
-#pragma unroll
-			for (int j = 0; j < 8; ++j) {
-				const uint32_t tw = j < 4 ? ta : tb;
-				const uint32_t x = tw >> (8 * (j & 3));
-				R.push(x & 3u, x >> 2);
-				const bool valid = R.valid();
-				tl += valid ? 1u : 0u;
-				const uint32_t widx = valid ? vc_filter_word(R.flo, R.rlo, fsh, A.wbits) : zero_word;
-				if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(widx)); fw[j] = 0u; }
-				else fw[j] = filt[widx];
-				fm[j] = vc_filter_mask(R.flo, R.rlo);
-				fl[j] = R.flo; fh[j] = R.fhi;
-			}
-#pragma unroll
-			for (int j = 0; j < 8; ++j) {
-				const bool hit = (fw[j] & fm[j]) == fm[j];
-				const uint64_t bal = __ballot(hit);
-				if constexpr ((ABL & 4) != 0) { asm volatile("" :: "s"(bal)); }
-				else if (bal) queue_append(A, Q, bal, hit, ((uint64_t)fh[j] << 32) | fl[j], lane);
-			}
-		}
-		w0 = w4; w1 = x1; w2 = x2; w3 = x3; w4 = x4;
-		x1 = y1; x2 = y2; x3 = y3; x4 = y4;
-		wi += 4;
-	}
-}
-
-// ---------------------------------------------------------------------------
-// packed-stream scan for compile-time k in 17..31 (the hot path)
-// ---------------------------------------------------------------------------
-//
-// Each 16-base chunk is packed once into 2-bit streams:
-//   L  little-endian codes, base j at bits 2j           (complemented: C = ~L)
-//   B  big-endian codes,    base j at bits 2(15-j)      (pair-reversed L)
-// The forward k-mer's low 32 bits at base j are one v_alignbit of (B[c-1]:B[c])
-// and the reverse complement's low 32 bits one v_alignbit of the C stream, with
-// compile-time shifts; the prefilter needs nothing else.  Filter passes set
-// bits of a per-lane 16-bit mask hm (bit 15-j <-> window ending at base j).
-//
-// Window validity is not tracked per base: per chunk, V (same bit order as
-// hm) holds the windows that lie inside [vlo, vhi) and contain no invalid
-// base; hm &= V.  Windows ending at base j are valid iff j >= L + K - 16c
-// (L = last invalid position before the chunk, vlo - 1 at the start) and
-// 16c + j < vhi; U = 16 - (L + K - 16c) and Qe = 16 - (vhi - 16c) are carried
-// per lane.  A chunk with an invalid base of its own (an N; rare) also
-// invalidates its windows from the first such base on and moves L to the last.
-// Only at the end of a chunk, and only if some lane of the wave has a hit,
-// are the full forward k-mers of the hit positions extracted (variable
-// shift) and queued.
-
-// 4x4 transpose of 2-bit fields: (byte r, field c) <-> (byte c, field r).
-__device__ __forceinline__ uint32_t transpose2x4x4(uint32_t a)
-{
-	uint32_t t = ((a >> 6) ^ a) & 0x00CC00CCu;
-	a ^= t ^ (t << 6);
-	t = ((a >> 12) ^ a) & 0x0000F0F0u;
-	a ^= t ^ (t << 12);
-	return a;
-}
-
-// Reverse the order of the 16 2-bit fields of a word.
-__device__ __forceinline__ uint32_t pairrev(uint32_t x)
-{
-	x = __builtin_bitreverse32(x);
-	return ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
-}
-
-__device__ __forceinline__ int clamp16(int v) { return v < 0 ? 0 : (v > 16 ? 16 : v); }
-
-// One 16-base chunk c of the packed scan from its five dwords (w0: the dword
-// holding the chunk's first byte, realigned by sh); (B1, C1) / (B2, C2) are
-// the streams of chunks c-1 / c-2 and move on to c / c-1.
-template <int K, int ABL>
-__device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int tail_c, uint32_t sh,
-                                             uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
-                                             uint32_t &Bm1, uint32_t &Bm2, uint32_t &Cm1, uint32_t &Cm2,
-                                             int &U, int &Qe, const uint32_t *__restrict__ filt, WaveQueue &Q,
-                                             uint32_t &tl, int lane)
-{
-	constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
-	const uint32_t fsh = A.fsh;
-	const uint32_t wmask4 = ((1u << A.wbits) - 1u) << 2;
-	const uint32_t fbase = lds_base(filt);       // the filter sits at a 16-byte aligned LDS base
-	const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
-	const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
-	const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
-	const uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
-	uint32_t t0 = dec_head(b0), t1 = dec_head(b1), t2 = dec_head(b2), t3 = dec_head(b3);
-	if (__ballot(c == tail_c)) {
-		if (c == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
-	}
-	U += 16;
-	Qe += 16;
-	// pack the chunk's codes: byte r of A holds bases r, 4+r, 8+r, 12+r
-	const uint32_t Am = (t0 & 0x03030303u) | ((t1 & 0x03030303u) << 2) |
-	                    ((t2 & 0x03030303u) << 4) | ((t3 & 0x03030303u) << 6);
-	const uint32_t L = transpose2x4x4(Am);          // base j at bits 2j
-	const uint32_t Cc = ~L;                          // complement codes, little-endian
-	const uint32_t Bc = pairrev(L);                  // big-endian codes
-
-	uint32_t hm = 0;                                 // filter pass, bit 15 - j for base j
-	// pass <=> bits (flo & 31) and (rlo & 31) of the filter word are set:
-	// hm = (hm << 1) | ((w >> flo) & (w >> rlo) & 1), 4 VALU per window
-	uint32_t fw[16], fl[16], rl[16];
-#pragma unroll
-	for (int j = 0; j < 16; ++j) {
-		const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, (uint32_t)(2 * (15 - j)));
-		const int s2 = j - K + 1 + 32;               // window start relative to chunk c-2
-		uint32_t rlo;
-		if (s2 >= 16) rlo = __builtin_amdgcn_alignbit(Cc, Cm1, (uint32_t)(2 * (s2 - 16)));
-		else rlo = __builtin_amdgcn_alignbit(Cm1, Cm2, (uint32_t)(2 * s2));
-		// byte address of word (mix >> fsh) & (2^wbits - 1): fsh >= 5 for k >= 17
-		const uint32_t wsh = vc_filter_mix(flo, rlo) >> (fsh - 2u);
-		if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(wsh)); fw[j] = wsh; }
-		else fw[j] = lds_word(fbase, wsh, wmask4);
-		fl[j] = flo;
-		rl[j] = rlo;
-	}
-#pragma unroll
-	for (int j = 0; j < 16; ++j)
-		hm = (hm << 1) | ((fw[j] >> (fl[j] & 31u)) & (fw[j] >> (rl[j] & 31u)) & 1u);
-	// windows of this chunk inside [vlo, vhi) with no earlier invalid base
-	uint32_t V = ((1u << clamp16(U)) - 1u) & ~((1u << clamp16(Qe)) - 1u);
-	const uint32_t anyinv = (t0 | t1 | t2 | t3) & 0x04040404u;
-	if (__ballot(anyinv != 0u)) {
-		if (anyinv != 0u) {
-			// invalid flags packed like the codes: base j at bit 2j of F
-			const uint32_t Im = ((t0 >> 2) & 0x01010101u) | (t1 & 0x04040404u) |
-			                    ((t2 << 2) & 0x10101010u) | ((t3 << 4) & 0x40404040u);
-			const uint32_t F = transpose2x4x4(Im);
-			const int j0 = (int)((uint32_t)__builtin_ctz(F) >> 1);          // first invalid base
-			const int j1 = (int)((31u - (uint32_t)__builtin_clz(F)) >> 1);  // last invalid base
-			V &= ~((2u << (15 - j0)) - 1u);          // windows ending at j >= j0
-			const int u1 = 16 - j1 - K;
-			U = U < u1 ? U : u1;
-		}
-	}
-	hm &= V;
-	tl += (uint32_t)__builtin_popcount(V);
-	// queue the hit positions' forward k-mers (bit b <-> base j = 15 - b)
-	if constexpr ((ABL & 4) != 0) {
-		asm volatile("" :: "v"(hm));
-	} else if (__ballot(hm != 0u)) {
-		for (;;) {
-			const bool has = hm != 0u;
-			const uint64_t bal = __ballot(has);
-			if (!bal) break;
-			// lowest pass first; lanes without one compute a garbage key they do not append
-			const uint32_t b = (uint32_t)__builtin_ctz(hm | 0x80000000u);   // hm < 2^16
-			const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, 2u * b);
-			const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
-			queue_append(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
-			hm &= hm - 1u;
-		}
-	}
-	Bm2 = Bm1; Bm1 = Bc;
-	Cm2 = Cm1; Cm1 = Cc;
-}
-
-// One global_load_dwordx4 of dwords [q, q+4), always exactly one load
-// instruction, so that the compiler can count loads in flight and wait only
-// for the quad a chunk is about to use.  A quad that would pass the end of
-// the buffer is loaded from its last four dwords instead (the host guarantees
-// at least four) and the return value says how far it was moved back; the
-// user shifts the dwords into place (quad_fix).  Dwords past the end of the
-// buffer are never part of a read.
-__device__ __forceinline__ uint32_t ldq(const uint32_t *__restrict__ s32, uint64_t q, uint64_t wmax,
-                                        uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
-{
-	const uint64_t lim = wmax - 3u;
-	const bool clamp = q > lim;
-	const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(s32 + (clamp ? lim : q));
-	a = v.x; b = v.y; c = v.z; d = v.w;
-	return clamp ? (q - lim > 3u ? 3u : (uint32_t)(q - lim)) : 0u;
-}
-
-__device__ __forceinline__ void quad_fix(uint32_t sft, uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
-{
-	if (__ballot(sft != 0u)) {       // only the last reads of a buffer
-		asm volatile("");            // keep this rare branch a branch
-		if (sft != 0u) {
-			a = sft == 1u ? b : (sft == 2u ? c : d);
-			b = sft == 1u ? c : d;
-			c = d;
-		}
-	}
-}
-
-// Chunks are processed in pairs.  The 8 dwords of the next pair are requested
-// (two dwordx4 from the same lines, back to back) while the current pair is
-// scanned, so each load has two chunks of work to hide behind.  The steady
-// loop issues the same loads on every trip (lanes past their span re-read
-// harmless bytes), the last pair is peeled: the compiler then waits for a
-// pair's data only when the pair starts.
-template <int K, bool HAS_LO, int ABL = 0>
-__device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
-                                                 uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
-                                                 int vlo, int vhi, int nit,
-                                                 const uint32_t *__restrict__ filt, WaveQueue &Q,
-                                                 uint32_t &tl, int lane)
-{
-	static_assert(K >= 17 && K <= 31, "packed scan needs 17 <= k <= 31");
-	const int tail_c = (len & 15) ? (len >> 4) : -1;
-
-	uint64_t addr = off + 16ull * (uint64_t)c_lo;
-	uint64_t wi = addr >> 2;
-	const uint32_t sh = (uint32_t)(addr & 3u);
-	uint32_t w0, w1, w2, w3, w4, w5, w6, w7, w8;
-	w0 = ldw(s32, wi, wmax);
-	uint32_t d1 = ldq(s32, wi + 1, wmax, w1, w2, w3, w4);
-	uint32_t d5 = ldq(s32, wi + 5, wmax, w5, w6, w7, w8);
-
-	uint32_t Bm1 = 0, Bm2 = 0, Cm1 = 0, Cm2 = 0;   // streams of the two previous chunks
-	int U = 1 - K - vlo + 16 * c_lo;                 // +16 at the top of every chunk
-	int Qe = -vhi + 16 * c_lo;
-
-	[[maybe_unused]] uint32_t abl_sink = 0;
-	int it = 0;
-	for (; it + 2 < nit; it += 2) {
-		const int c = c_lo + it;
-		uint32_t n0, n1, n2, n3, n4, n5, n6, n7, dn0, dn4;
-		if constexpr ((ABL & 2) != 0) {
-			n0 = (uint32_t)wi * 0x9E3779B1u; n1 = n0 ^ 0x41434754u; n2 = n0 + 0x54474341u; n3 = n0 * 5u;
-			n4 = n0 ^ 0x5A5A5A5Au; n5 = n1 + 7u; n6 = n2 ^ n3; n7 = n4 * 3u;
-			dn0 = dn4 = 0;
-		} else if constexpr ((ABL & 16) != 0) {
-			// timing experiment: issue the real loads but consume them only
-			// after the scan (isolates the cost of waiting from issuing)
-			uint32_t t0_, t1_, t2_, t3_, t4_, t5_, t6_, t7_;
-			ldq(s32, wi + 9, wmax, t0_, t1_, t2_, t3_);
-			ldq(s32, wi + 13, wmax, t4_, t5_, t6_, t7_);
-			abl_sink ^= t0_ ^ t1_ ^ t2_ ^ t3_ ^ t4_ ^ t5_ ^ t6_ ^ t7_;
-			n0 = (uint32_t)wi * 0x9E3779B1u; n1 = n0 ^ 0x41434754u; n2 = n0 + 0x54474341u; n3 = n0 * 5u;
-			n4 = n0 ^ 0x5A5A5A5Au; n5 = n1 + 7u; n6 = n2 ^ n3; n7 = n4 * 3u;
-			dn0 = dn4 = 0;
-		} else if constexpr ((ABL & 8) != 0) {
-			// timing experiment: the memory pattern of a wave-tiled layout
-			// (chunk c of lane l at 16 * (64 c + l) from a wave base)
-			const uint64_t tb = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(off >> 4)) << 2) +
-			                    (uint64_t)(64 * (it + 2) + lane) * 4u;
-			dn0 = ldq(s32, tb, wmax, n0, n1, n2, n3);
-			dn4 = ldq(s32, tb + 256, wmax, n4, n5, n6, n7);
-		} else {
-			dn0 = ldq(s32, wi + 9, wmax, n0, n1, n2, n3);
-			dn4 = ldq(s32, wi + 13, wmax, n4, n5, n6, n7);
-		}
-		quad_fix(d1, w1, w2, w3, w4);
-		quad_fix(d5, w5, w6, w7, w8);
-		packed_chunk<K, ABL>(A, c, tail_c, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
-		packed_chunk<K, ABL>(A, c + 1, tail_c, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
-		w0 = w8;
-		w1 = n0; w2 = n1; w3 = n2; w4 = n3; d1 = dn0;
-		w5 = n4; w6 = n5; w7 = n6; w8 = n7; d5 = dn4;
-		wi += 8;
-	}
-	if constexpr ((ABL & 16) != 0) tl += abl_sink & 1u;
-	if (it < nit) {
-		const int c = c_lo + it;
-		quad_fix(d1, w1, w2, w3, w4);
-		quad_fix(d5, w5, w6, w7, w8);
-		packed_chunk<K, ABL>(A, c, tail_c, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
-		if (it + 1 < nit)
-			packed_chunk<K, ABL>(A, c + 1, tail_c, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl,
-			                     lane);
-	}
-}
-
-// k in 17..31 with a compile-time specialisation: packed streams; otherwise
-// the general rolling scan.
-template <int K, bool HAS_LO, int ABL = 0>
-__device__ __forceinline__ void scan_any(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
-                                         uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
-                                         int vlo, int vhi, int nit, const uint32_t *__restrict__ filt,
-                                         WaveQueue &Q, uint32_t &tl, int lane)
-{
-	if constexpr (K >= 17)
-		scan_span_packed<K, HAS_LO, ABL>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl, lane);
-	else
-		scan_span<K, HAS_LO, ABL>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl, lane);
-}
-
-__device__ __forceinline__ void load_filter(const VcKernelArgs &A, uint32_t *filt)
-{
-	const uint32_t nw = 1u << A.wbits;
-	const uint4 *src = reinterpret_cast<const uint4 *>(A.filter);
-	uint4 *dst = reinterpret_cast<uint4 *>(filt);
-	for (uint32_t i = threadIdx.x; i < nw / 4u; i += blockDim.x) dst[i] = src[i];
-	if (threadIdx.x < 4) filt[nw + threadIdx.x] = 0u;     // the zero word(s)
-	__syncthreads();
-}
-
-// ---------------------------------------------------------------------------
-// kernel 1: whole reads, one lane per read
-// ---------------------------------------------------------------------------
-
-template <int K, int ABL = 0>
-__global__ void __launch_bounds__(VC_BLOCK)
-vc_count_reads_kernel(VcKernelArgs A)
-{
-	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-	uint32_t *filt = smem;
-	const int lane = threadIdx.x & (WAVE - 1);
-	const int wave = threadIdx.x / WAVE;
-	WaveQueue Q;
-	Q.q = reinterpret_cast<uint64_t *>(smem + vc_filter_lds_words(A.wbits)) + wave * VC_QCAP;
-	Q.n = 0;
-	load_filter(A, filt);
-
-	const uint32_t *s32 = reinterpret_cast<const uint32_t *>(A.seq);
-	const uint64_t wmax = A.seq_words ? A.seq_words - 1 : 0;
-	unsigned long long tally = 0;
-
-	// The lengths and offsets of the next read group are requested before
-	// this group is scanned (one load each, index clamped, so the compiler's
-	// count of loads in flight stays exact) and used after its queue drain.
-	const uint64_t rlast = A.n_reads - 1;
-	uint64_t g = blockIdx.x;
-	uint64_t r = g * (uint64_t)VC_BLOCK + threadIdx.x;
-	uint32_t len_raw = A.lens[r < rlast ? r : rlast];
-	uint64_t off_raw = A.offs[r < rlast ? r : rlast];
-	while (g * (uint64_t)VC_BLOCK < A.n_reads) {
-		int len = r < A.n_reads ? (int)len_raw : 0;
-		const uint64_t off = off_raw + A.off_adj;
-		if ((uint32_t)len > VC_LONG_READ) {
-			const uint32_t slot = atomicAdd(A.nlong, 1u);
-			if (slot < A.long_cap) A.longlist[slot] = (uint32_t)r;
-			len = 0;
-		}
-		const uint64_t gn = g + gridDim.x;
-		const uint64_t rn = gn * (uint64_t)VC_BLOCK + threadIdx.x;
-		len_raw = A.lens[rn < rlast ? rn : rlast];
-		off_raw = A.offs[rn < rlast ? rn : rlast];
-		const int nch = (len + 15) >> 4;
-		const int nit = wave_max_i32(nch);
-		uint32_t tl = 0;
-		scan_any<K, false, ABL>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tl, lane);
-		tally += tl;
-		queue_flush(A, Q, lane);     // one drain per read group, probes overlapped
-		g = gn;
-		r = rn;
-	}
-	queue_flush(A, Q, lane);
-	const unsigned long long t = wave_sum_u64(tally);
-	if (lane == 0 && t) atomicAdd(A.tally, t);
-}
-
-// ---------------------------------------------------------------------------
-// kernel 2: long reads, every lane of the grid takes one segment
-// ---------------------------------------------------------------------------
-
-template <int K>
-__global__ void __launch_bounds__(VC_BLOCK)
-vc_count_long_kernel(VcKernelArgs A)
-{
-	const uint32_t nl_raw = *A.nlong;
-	const uint32_t nl = nl_raw < A.long_cap ? nl_raw : A.long_cap;
-	if (nl == 0) return;   // uniform over the grid
-	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-	uint32_t *filt = smem;
-	const int lane = threadIdx.x & (WAVE - 1);
-	const int wave = threadIdx.x / WAVE;
-	WaveQueue Q;
-	Q.q = reinterpret_cast<uint64_t *>(smem + vc_filter_lds_words(A.wbits)) + wave * VC_QCAP;
-	Q.n = 0;
-	load_filter(A, filt);
-
-	const uint32_t *s32 = reinterpret_cast<const uint32_t *>(A.seq);
-	const uint64_t wmax = A.seq_words ? A.seq_words - 1 : 0;
-	const int k = K ? K : A.k;
-	unsigned long long tally = 0;
-	const uint64_t stride = (uint64_t)gridDim.x * VC_BLOCK;
-
-	for (uint32_t li = 0; li < nl; ++li) {
-		const uint32_t r = A.longlist[li];
-		const int len = (int)A.lens[r];
-		const uint64_t off = A.offs[r] + A.off_adj;
-		const uint64_t nseg = ((uint64_t)len + VC_LONG_SEG - 1) / VC_LONG_SEG;
-		for (uint64_t s0 = (uint64_t)blockIdx.x * VC_BLOCK; s0 < nseg; s0 += stride) {
-			const uint64_t s = s0 + threadIdx.x;
-			int vlo = 0, vhi = 0, c_lo = 0, c_hi = 0;
-			if (s < nseg) {
-				const int64_t e0 = (int64_t)s * VC_LONG_SEG;
-				const int64_t e1 = e0 + VC_LONG_SEG < len ? e0 + VC_LONG_SEG : len;
-				vlo = (int)(e0 - (k - 1) > 0 ? e0 - (k - 1) : 0);
-				vhi = (int)e1;
-				c_lo = vlo >> 4;
-				c_hi = (vhi + 15) >> 4;
-			}
-			const int nit = wave_max_i32(c_hi - c_lo);
-			uint32_t tl = 0;
-			scan_any<K, true>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl, lane);
-			tally += tl;
-		}
-	}
-	queue_flush(A, Q, lane);
-	const unsigned long long t = wave_sum_u64(tally);
-	if (lane == 0 && t) atomicAdd(A.tally, t);
-}
+#define VC_K_LIST(X) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) \
+	X(30) X(31)
+#define VC_K_DECL(k)                                                                         \
+	hipError_t vc_launch_k##k(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st); \
+	hipError_t vc_setup_k##k(int lds);
+VC_K_LIST(VC_K_DECL)
+#undef VC_K_DECL
 
 // ---------------------------------------------------------------------------
 // debug kernel: position-dependent decode of whole reads (tests only)
@@ -903,73 +104,23 @@ __global__ void vc_synth_kernel(uint8_t *seq, uint64_t *offs, uint32_t *lens, ui
 // launchers
 // ---------------------------------------------------------------------------
 
-template <int K, int ABL = 0>
-static hipError_t launch_kw(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
-{
-	const size_t lds = vc_lds_bytes(A->wbits);
-	hipLaunchKernelGGL((vc_count_reads_kernel<K, ABL>), dim3(grid), dim3(VC_BLOCK), lds, st, *A);
-	hipError_t e = hipGetLastError();
-	if (e != hipSuccess) return e;
-	hipLaunchKernelGGL((vc_count_long_kernel<K>), dim3(grid_long), dim3(VC_BLOCK), lds, st, *A);
-	return hipGetLastError();
-}
-
-#ifdef VC_ABLATION
-#define VC_ABL_LIST(X) X(1) X(2) X(4) X(3) X(5) X(6) X(7) X(8) X(12) X(16) X(20)
-#endif
-
-template <int K>
-static hipError_t launch_k(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
-{
-#ifdef VC_ABLATION
-	if (K == 21 && A->ablate) {
-		switch (A->ablate) {
-#define VC_ABL_CASE(n) case n: return launch_kw<21, n>(A, grid, grid_long, st);
-			VC_ABL_LIST(VC_ABL_CASE)
-#undef VC_ABL_CASE
-		default: break;
-		}
-	}
-#endif
-	return launch_kw<K>(A, grid, grid_long, st);
-}
-
 extern "C" hipError_t vc_launch_count(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
 {
 	switch (A->k) {
-	case 21: return launch_k<21>(A, grid, grid_long, st);
-	case 31: return launch_k<31>(A, grid, grid_long, st);
+#define VC_K_CASE(k) case k: return vc_launch_k##k(A, grid, grid_long, st);
+		VC_K_LIST(VC_K_CASE)
+#undef VC_K_CASE
 	default: return launch_k<0>(A, grid, grid_long, st);
 	}
-}
-
-template <int K>
-static hipError_t setup_k(int lds)
-{
-	hipError_t e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<K>,
-	                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-	if (e == hipSuccess)
-		e = hipFuncSetAttribute((const void *)vc_count_long_kernel<K>,
-		                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-#ifdef VC_ABLATION
-	if (K == 21) {
-#define VC_ABL_SET(n)                                                                           \
-	if (e == hipSuccess)                                                                        \
-		e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<21, n>,                     \
-		                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-		VC_ABL_LIST(VC_ABL_SET)
-#undef VC_ABL_SET
-	}
-#endif
-	return e;
 }
 
 extern "C" hipError_t vc_kernel_setup(void)
 {
 	const int lds = (int)vc_lds_bytes(VC_MAX_FILTER_WBITS);
-	hipError_t e = setup_k<21>(lds);
-	if (e == hipSuccess) e = setup_k<31>(lds);
-	if (e == hipSuccess) e = setup_k<0>(lds);
+	hipError_t e = setup_k<0>(lds);
+#define VC_K_SET(k) if (e == hipSuccess) e = vc_setup_k##k(lds);
+	VC_K_LIST(VC_K_SET)
+#undef VC_K_SET
 	return e;
 }
 

@@ -119,8 +119,10 @@ def test_python_mirror_matches_reference(name, manifest, synth_dir, tmp_path):
 # kernels vs oracle on random inputs
 # --------------------------------------------------------------------------
 
-@pytest.mark.parametrize("k", [1, 5, 15, 16, 17, 21, 24, 31])
+@pytest.mark.parametrize("k", [1, 5, 15] + list(range(16, 32)))
 def test_random_reads_vs_oracle(k):
+    """Every k of the packed path (16..31, one kernel instantiation each) and the
+    run-time-k kernel (k < 16)."""
     rng = np.random.default_rng(k)
     lens = list(rng.integers(0, 200, 3000)) + [0, 1, k - 1, k, k + 1, 15, 16, 17, 31, 32, 33, 150, 151, 1000, 5000]
     reads = random_reads(rng, lens)
@@ -132,7 +134,7 @@ def test_random_reads_vs_oracle(k):
     assert int(want.sum()) > 0
 
 
-@pytest.mark.parametrize("k", [21, 31, 9])
+@pytest.mark.parametrize("k", [21, 31, 9, 16, 26])
 def test_long_reads_segmented_kernel(k):
     """Reads > VC_LONG_READ (16384) take the segmented long-read kernel."""
     rng = np.random.default_rng(77 + k)
@@ -143,6 +145,22 @@ def test_long_reads_segmented_kernel(k):
     want, km_want = oracle_counts(k, keys, vals, n_pat, reads)
     assert km == km_want
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("k,n_sel", [(16, 65336), (16, 65337), (27, 65337), (31, 90000)])
+def test_second_level_filter_threshold(k, n_sel):
+    """Tables of > 65536 keys (VC_L2F_MIN_KEYS) also build the second-level filter;
+    either side of the threshold must count identically to the oracle."""
+    rng = np.random.default_rng(1000 + k + n_sel)
+    reads = [np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, int(L))].tobytes()
+             for L in rng.integers(100, 300, 1500)]
+    keys, vals, n_pat = table_from_reads(k, reads, rng, n_pat=n_sel)
+    assert keys.size == n_sel + 200
+    got, km = gpu_counts(k, keys, vals, n_pat, reads, blocks=2)
+    want, km_want = oracle_counts(k, keys, vals, n_pat, reads)
+    assert km == km_want
+    assert np.array_equal(got, want)
+    assert int(want.sum()) > 50_000
 
 
 @pytest.mark.parametrize("k", [1, 5, 15, 16, 17, 21, 31])
