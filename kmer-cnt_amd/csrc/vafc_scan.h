@@ -595,6 +595,21 @@ __device__ __forceinline__ uint32_t ldq(const uint32_t *__restrict__ s32, uint64
 	return clamp ? (q - lim > 3u ? 3u : (uint32_t)(q - lim)) : 0u;
 }
 
+// Unclamped load for read groups whose every load is known to lie inside
+// the buffer (checked once per group, see vc_count_reads_kernel).
+template <bool SAFE>
+__device__ __forceinline__ uint32_t ldq_s(const uint32_t *__restrict__ s32, uint64_t q, uint64_t wmax,
+                                          uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
+{
+	if constexpr (SAFE) {
+		const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(s32 + q);
+		a = v.x; b = v.y; c = v.z; d = v.w;
+		return 0u;
+	} else {
+		return ldq(s32, q, wmax, a, b, c, d);
+	}
+}
+
 __device__ __forceinline__ void quad_fix(uint32_t sft, uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
 {
 	if (__ballot(sft != 0u)) {       // only the last reads of a buffer
@@ -613,7 +628,7 @@ __device__ __forceinline__ void quad_fix(uint32_t sft, uint32_t &a, uint32_t &b,
 // loop issues the same loads on every trip (lanes past their span re-read
 // harmless bytes), the last pair is peeled: the compiler then waits for a
 // pair's data only when the pair starts.
-template <int K, bool HAS_LO, int ABL = 0>
+template <int K, bool HAS_LO, int ABL = 0, bool SAFE = false>
 __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
                                                  uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
                                                  int vlo, int vhi, int nit,
@@ -627,9 +642,9 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	uint64_t wi = addr >> 2;
 	const uint32_t sh = (uint32_t)(addr & 3u);
 	uint32_t w0, w1, w2, w3, w4, w5, w6, w7, w8;
-	w0 = ldw(s32, wi, wmax);
-	uint32_t d1 = ldq(s32, wi + 1, wmax, w1, w2, w3, w4);
-	uint32_t d5 = ldq(s32, wi + 5, wmax, w5, w6, w7, w8);
+	w0 = SAFE ? s32[wi] : ldw(s32, wi, wmax);
+	uint32_t d1 = ldq_s<SAFE>(s32, wi + 1, wmax, w1, w2, w3, w4);
+	uint32_t d5 = ldq_s<SAFE>(s32, wi + 5, wmax, w5, w6, w7, w8);
 
 	uint32_t Bm1 = 0, Bm2 = 0, Cm1 = 0, Cm2 = 0;   // streams of the two previous chunks
 	int U = 1 - K - vlo + 16 * c_lo;                 // +16 at the top of every chunk
@@ -662,8 +677,8 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 			dn0 = ldq(s32, tb, wmax, n0, n1, n2, n3);
 			dn4 = ldq(s32, tb + 256, wmax, n4, n5, n6, n7);
 		} else {
-			dn0 = ldq(s32, wi + 9, wmax, n0, n1, n2, n3);
-			dn4 = ldq(s32, wi + 13, wmax, n4, n5, n6, n7);
+			dn0 = ldq_s<SAFE>(s32, wi + 9, wmax, n0, n1, n2, n3);
+			dn4 = ldq_s<SAFE>(s32, wi + 13, wmax, n4, n5, n6, n7);
 		}
 		quad_fix(d1, w1, w2, w3, w4);
 		quad_fix(d5, w5, w6, w7, w8);
@@ -688,14 +703,15 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 
 // k in 16..31 with a compile-time specialisation: packed streams; otherwise
 // the general rolling scan.
-template <int K, bool HAS_LO, int ABL = 0>
+template <int K, bool HAS_LO, int ABL = 0, bool SAFE = false>
 __device__ __forceinline__ void scan_any(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
                                          uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
                                          int vlo, int vhi, int nit, const uint32_t *__restrict__ filt,
                                          WaveQueue &Q, uint32_t &tl, int lane)
 {
 	if constexpr (K >= 16)
-		scan_span_packed<K, HAS_LO, ABL>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl, lane);
+		scan_span_packed<K, HAS_LO, ABL, SAFE>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl,
+		                                       lane);
 	else
 		scan_span<K, HAS_LO, ABL>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl, lane);
 }
@@ -754,7 +770,14 @@ vc_count_reads_kernel(VcKernelArgs A)
 		const int nch = (len + 15) >> 4;
 		const int nit = wave_max_i32(nch);
 		uint32_t tl = 0;
-		scan_any<K, false, ABL>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tl, lane);
+		// the packed scan loads dwords [off/4, off/4 + 8 ceil(nit/2) + 9) (lanes
+		// past their span keep loading); groups clear of the buffer end skip the
+		// per-load clamping
+		const bool clear = (off >> 2) + 8u * (uint64_t)((nit + 1) >> 1) + 9u <= wmax;
+		if (K >= 16 && __builtin_amdgcn_ballot_w64(!clear) == 0)
+			scan_any<K, false, ABL, true>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tl, lane);
+		else
+			scan_any<K, false, ABL>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tl, lane);
 		tally += tl;
 		queue_flush(A, Q, lane);     // one drain per read group, probes overlapped
 		g = gn;

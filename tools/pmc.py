@@ -42,6 +42,8 @@ def main():
     passes = PASSES
     if rest[:2] == ["--set", "diag"]:
         passes, rest = DIAG, rest[2:]
+    elif rest[:2] == ["--set", "insts"]:      # instruction mix only (one pass)
+        passes, rest = PASSES[:1], rest[2:]
     bench_args = rest or ["--steps", "2", "--warmup", "1", "--no-cpu"]
     os.makedirs(out, exist_ok=True)
     acc = {}
