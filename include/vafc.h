@@ -152,9 +152,11 @@ typedef struct {
  * under the reference's block loop: blocks of >= block_bases bases, reads
  * shorter than k skipped, a read error (-2) or EOF ends a block, the file ends
  * at the third empty block (vaf-counter.c:486-517, kthread.c:97-128).  Reads
- * are streamed to the device in large pinned batches.  n_threads is accepted
- * for CLI parity (-t).  Returns VC_EIO if the file cannot be opened (the
- * reference skips such files silently, vaf-counter.c:557). */
+ * are streamed to the device in large pinned batches.  Plain (uncompressed)
+ * files of 32 MB or more are parsed by n_threads worker threads (the CLI's
+ * -t; vafc_ingest.h) with identical results; gzip and small files use one
+ * reader thread.  Returns VC_EIO if the file cannot be opened (the reference
+ * skips such files silently, vaf-counter.c:557). */
 int vc_count_file(vc_ctx *ctx, const char *path, int block_bases, int n_threads,
                   vc_file_stats *st);
 
@@ -164,6 +166,15 @@ int vc_count_file(vc_ctx *ctx, const char *path, int block_bases, int n_threads,
  * GPU and measures host ingest speed. */
 int vc_scan_file(const char *path, int k, int block_bases, vc_file_stats *st,
                  uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out, size_t lens_cap);
+
+/* Host-only: vc_count_file's parallel reader for plain (uncompressed) files,
+ * without a device: n_threads workers parse pieces of piece_bytes of the file
+ * concurrently (vafc_ingest.h); accepted reads come out in file order, exactly
+ * as vc_scan_file's.  Lets the parallel reader be checked without a GPU and
+ * measures its speed.  gzip input is rejected (VC_EINVAL). */
+int vc_scan_file_parallel(const char *path, int k, int block_bases, int n_threads, uint64_t piece_bytes,
+                          vc_file_stats *st, uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out,
+                          size_t lens_cap);
 
 /* Host-only: the kseq_read return value of every record until -1 (inclusive),
  * written while they fit; returns the number of calls made, or VC_EIO. */

@@ -3,6 +3,8 @@
 
 #include <ctype.h>
 #include <stdlib.h>
+#include <errno.h>
+#include <unistd.h>
 
 bool VcFastqReader::open(const char *path, size_t window)
 {
@@ -18,10 +20,24 @@ bool VcFastqReader::open(const char *path, size_t window)
 	return buf_ != nullptr;
 }
 
+bool VcFastqReader::open_fd(int fd, uint64_t off, size_t window)
+{
+	close();
+	fd_ = fd;
+	foff_ = base_ = off;
+	cap_ = window;
+	buf_ = (uint8_t *)malloc(cap_);
+	b_ = e_ = 0;
+	eof_ = false;
+	hdr_ = 0;
+	return buf_ != nullptr;
+}
+
 void VcFastqReader::close()
 {
 	if (fp_) gzclose(fp_);
 	fp_ = nullptr;
+	fd_ = -1;
 	free(buf_);
 	buf_ = nullptr;
 }
@@ -29,7 +45,14 @@ void VcFastqReader::close()
 bool VcFastqReader::refill()
 {
 	if (eof_) return false;
-	int n = gzread(fp_, buf_, (unsigned)cap_);
+	ssize_t n;
+	if (fd_ >= 0) {
+		do n = pread(fd_, buf_, cap_, (off_t)foff_); while (n < 0 && errno == EINTR);
+		base_ = foff_;
+		if (n > 0) foff_ += (uint64_t)n;
+	} else {
+		n = gzread(fp_, buf_, (unsigned)cap_);
+	}
 	if (n <= 0) {
 		eof_ = true;
 		b_ = e_ = 0;
@@ -38,6 +61,18 @@ bool VcFastqReader::refill()
 	b_ = 0;
 	e_ = (size_t)n;
 	return true;
+}
+
+int64_t VcFastqReader::peek_header()
+{
+	if (!hdr_) {   // the scan of next() (kseq.h:197-201)
+		int c;
+		do c = getc_(); while (c != -1 && c != '>' && c != '@');
+		if (c == -1) return -1;
+		hdr_ = c;
+		hdr_pos_ = last_pos();
+	}
+	return (int64_t)hdr_pos_;
 }
 
 // Bytes up to the next '\n' (consumed, not stored) appended to dst; -1 only
@@ -99,11 +134,7 @@ void VcFastqReader::skip_line()
 int VcFastqReader::next()
 {
 	int c, d;
-	if (!hdr_) { // scan to a '>' or '@' (kseq.h:197-201)
-		do c = getc_(); while (c != -1 && c != '>' && c != '@');
-		if (c == -1) return -1;
-		hdr_ = c;
-	}
+	if (!hdr_ && peek_header() < 0) return -1;   // scan to a '>' or '@' (kseq.h:197-201)
 	seq_.l = qual_.l = 0;
 	if (token(&d) < 0) return -1;
 	if (d != '\n' && !at_end()) skip_line();          // comment (kseq.h:204)
@@ -113,7 +144,10 @@ int VcFastqReader::next()
 		seq_.push(c);
 		line(&seq_);
 	}
-	if (c == '>' || c == '@') hdr_ = c;
+	if (c == '>' || c == '@') {
+		hdr_ = c;
+		hdr_pos_ = last_pos();
+	}
 	if (c != '+') return (int)seq_.l;                 // FASTA
 	do c = getc_(); while (c != -1 && c != '\n');     // rest of the '+' line
 	if (c == -1) return -2;

@@ -42,17 +42,29 @@ public:
 	VcFastqReader() = default;
 	~VcFastqReader() { close(); }
 	bool open(const char *path, size_t window = (size_t)4 << 20);
+	// Plain-file source for the parallel ingest: records from file offset
+	// `off` of an open descriptor (read with pread, the descriptor is not
+	// owned).  `off` must be where kseq would look for a record's header.
+	bool open_fd(int fd, uint64_t off, size_t window = (size_t)4 << 20);
 	void close();
 	int next();
+	// File offset of the next record's header character ('@' or '>'),
+	// scanning forward like next() does; -1 at end of input.  next() then
+	// parses that record.
+	int64_t peek_header();
 	const char *seq() const { return seq_.s; }
 	size_t seq_len() const { return seq_.l; }
 
 private:
 	gzFile fp_ = nullptr;
+	int fd_ = -1;                 // pread source (open_fd), not owned
+	uint64_t foff_ = 0;           // file offset of the next pread
+	uint64_t base_ = 0;           // file offset of buf_[0] (pread source)
 	uint8_t *buf_ = nullptr;
 	size_t cap_ = 0, b_ = 0, e_ = 0;
 	bool eof_ = false;
 	int hdr_ = 0;                 // header char already consumed, 0 if none
+	uint64_t hdr_pos_ = 0;        // its file offset (pread source)
 	VcByteBuf seq_, qual_;
 
 	bool refill();
@@ -61,6 +73,7 @@ private:
 		if (b_ >= e_ && !refill()) return -1;
 		return buf_[b_++];
 	}
+	inline uint64_t last_pos() const { return base_ + b_ - 1; }   // of the byte getc_ just returned
 	inline bool at_end() { return b_ >= e_ && !refill(); }
 	int line(VcByteBuf *dst);     // rest of a line, appended; CR rule on the whole string
 	int token(int *delim);        // up to an isspace() byte, discarded

@@ -10,8 +10,11 @@
 // kernels in vafc_kernels.hip, and any HIP failure is returned as VC_EHIP.
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
 #include <limits.h>
 #include <math.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -22,6 +25,7 @@
 #include "vafc.h"
 #include "vafc_common.h"
 #include "vafc_fastq.h"
+#include "vafc_ingest.h"
 #include "vafc_internal.h"
 
 #define HIPCK(call)                                                                         \
@@ -247,6 +251,7 @@ struct vc_ctx {
 	uint32_t long_cap = 0;
 	Slot slot[2];
 	int cur = 0;
+	std::vector<Slot> islot;               // parallel ingest (vc_count_file on plain files)
 	bool timing = false, timed = false;
 	hipEvent_t t0 = nullptr, t1 = nullptr;
 };
@@ -391,6 +396,10 @@ extern "C" void vc_destroy(vc_ctx *c)
 	(void)hipSetDevice(c->dev);
 	if (c->st) (void)hipStreamSynchronize(c->st);
 	for (auto &s : c->slot) {
+		free_slot(s);
+		if (s.done) (void)hipEventDestroy(s.done);
+	}
+	for (auto &s : c->islot) {
 		free_slot(s);
 		if (s.done) (void)hipEventDestroy(s.done);
 	}
@@ -691,14 +700,135 @@ static int block_loop(VcFastqReader &rd, int k, int block_bases, Sink &&sink, vc
 	return rc;
 }
 
+// ---------------------------------------------------------------------------
+// parallel ingest of plain files (vafc_ingest.h): pieces parsed by -t worker
+// threads straight into pinned slots, shipped to the device in file order
+// ---------------------------------------------------------------------------
+
+#ifndef VC_PIECE_BYTES
+#define VC_PIECE_BYTES ((uint64_t)8 << 20)
+#endif
+
+namespace {
+
+class DeviceSink : public VcIngestSink {
+public:
+	explicit DeviceSink(vc_ctx *c) : c_(c) {}
+	int acquire(int slot, VcSlotBuf *b) override
+	{
+		HIPCK(hipSetDevice(c_->dev));
+		Slot &s = c_->islot[(size_t)slot];
+		if (s.pending) {
+			HIPCK(hipEventSynchronize(s.done));
+			s.pending = false;
+		}
+		if (!s.h_seq) {
+			int rc = slot_reserve(s, VC_PIECE_BYTES + VC_PIECE_BYTES / 4, VC_PIECE_BYTES / 64 + 1024);
+			if (rc != VC_OK) return rc;
+		}
+		fill(s, b);
+		return VC_OK;
+	}
+	int grow(int slot, VcSlotBuf *b, size_t bytes, size_t reads, size_t used_bytes, size_t used_reads) override
+	{
+		HIPCK(hipSetDevice(c_->dev));
+		Slot &s = c_->islot[(size_t)slot];
+		Slot n;
+		n.done = s.done;
+		if (hipHostMalloc(&n.h_seq, bytes, hipHostMallocDefault) != hipSuccess ||
+		    hipHostMalloc(&n.h_offs, reads * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
+		    hipHostMalloc(&n.h_lens, reads * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+		    hipMalloc(&n.d_seq, bytes) != hipSuccess || hipMalloc(&n.d_offs, reads * sizeof(uint64_t)) != hipSuccess ||
+		    hipMalloc(&n.d_lens, reads * sizeof(uint32_t)) != hipSuccess) {
+			free_slot(n);
+			return VC_EHIP;
+		}
+		n.cap_bytes = bytes;
+		n.cap_reads = reads;
+		memcpy(n.h_seq, s.h_seq, used_bytes);
+		memcpy(n.h_offs, s.h_offs, used_reads * sizeof(uint64_t));
+		memcpy(n.h_lens, s.h_lens, used_reads * sizeof(uint32_t));
+		free_slot(s);
+		s = n;
+		fill(s, b);
+		return VC_OK;
+	}
+	int submit(int slot, const VcSlotBuf &, uint64_t n, uint64_t bytes) override
+	{
+		Slot &s = c_->islot[(size_t)slot];
+		HIPCK(hipMemcpyAsync(s.d_seq, s.h_seq, bytes, hipMemcpyHostToDevice, c_->st));
+		HIPCK(hipMemcpyAsync(s.d_offs, s.h_offs, n * sizeof(uint64_t), hipMemcpyHostToDevice, c_->st));
+		HIPCK(hipMemcpyAsync(s.d_lens, s.h_lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, c_->st));
+		int rc = launch(c_, s.d_seq, bytes, s.d_offs, s.d_lens, n, c_->st);
+		if (rc != VC_OK) return rc;
+		HIPCK(hipEventRecord(s.done, c_->st));
+		s.pending = true;
+		return VC_OK;
+	}
+
+private:
+	vc_ctx *c_;
+	static void fill(const Slot &s, VcSlotBuf *b)
+	{
+		b->seq = s.h_seq;
+		b->offs = s.h_offs;
+		b->lens = s.h_lens;
+		b->cap_bytes = s.cap_bytes;
+		b->cap_reads = s.cap_reads;
+	}
+};
+
+} // namespace
+
+// Plain files of at least this size take the parallel reader.
+#ifndef VC_PARALLEL_MIN_BYTES
+#define VC_PARALLEL_MIN_BYTES ((uint64_t)32 << 20)
+#endif
+
+static int count_file_parallel(vc_ctx *c, int fd, uint64_t size, int block_bases, int n_threads,
+                               vc_file_stats &st)
+{
+	const int threads = n_threads < 1 ? 1 : (n_threads > 64 ? 64 : n_threads);
+	const int slots = threads + 2;
+	if (c->islot.size() < (size_t)slots) {
+		HIPCK(hipStreamSynchronize(c->st));
+		const size_t old = c->islot.size();
+		c->islot.resize((size_t)slots);
+		for (size_t i = old; i < c->islot.size(); ++i)
+			HIPCK(hipEventCreateWithFlags(&c->islot[i].done, hipEventDisableTiming));
+	}
+	DeviceSink sink(c);
+	const char *pe = getenv("VAFC_INGEST_PIECE");          // test knob: piece size in bytes
+	const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : VC_PIECE_BYTES;
+	return vc_ingest_plain(fd, size, c->k, block_bases, threads, slots, piece, sink, st);
+}
+
 extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n_threads,
                              vc_file_stats *st)
 {
-	(void)n_threads;
 	if (!c || !path) return VC_EINVAL;
 	vc_file_stats local = {0, 0, 0, 0.0};
 	const double t0 = wall_now();
 	HIPCK(hipSetDevice(c->dev));
+	{
+		const int fd = open(path, O_RDONLY);
+		if (fd < 0) return VC_EIO;
+		struct stat sb;
+		uint8_t magic[2] = {0, 0};
+		const bool plain = fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode) &&
+		                   !(pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b);
+		const char *me = getenv("VAFC_INGEST_MIN");        // test knob: smallest file for the parallel reader
+		const uint64_t min_bytes = me ? (uint64_t)atoll(me) : VC_PARALLEL_MIN_BYTES;
+		if (plain && (uint64_t)sb.st_size >= min_bytes && sb.st_size > 0) {
+			int rc = count_file_parallel(c, fd, (uint64_t)sb.st_size, block_bases, n_threads, local);
+			close(fd);
+			if (rc == VC_OK) HIPCK(hipStreamSynchronize(c->st));
+			local.seconds = wall_now() - t0;
+			if (st) *st = local;
+			return rc;
+		}
+		close(fd);
+	}
 	VcFastqReader rd;
 	if (!rd.open(path)) return VC_EIO;
 	BatchWriter bw(c);

@@ -1,0 +1,387 @@
+// vafc_ingest.cpp -- see vafc_ingest.h.
+#include "vafc_ingest.h"
+
+#include <errno.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "vafc_fastq.h"
+
+namespace {
+
+struct Piece {
+	uint64_t a = 0, b = 0;        // nominal byte range [a, b)
+	int64_t start = -1;           // header offset parsing began at; -1: no record found
+	uint64_t end = 0;             // header offset of the first record at or past b; size at EOF
+	bool eof = false;             // the reader hit end of input inside this piece
+	uint64_t n = 0, bytes = 0;    // accepted reads (len >= k) in the slot, their bases
+	std::vector<uint64_t> errs;   // a -2 came after this many accepted reads
+	VcSlotBuf buf;
+	int rc = VC_OK;
+	bool ready = false;
+};
+
+ssize_t pread_full(int fd, uint8_t *p, size_t n, uint64_t off)
+{
+	size_t got = 0;
+	while (got < n) {
+		ssize_t r = pread(fd, p + got, n - got, (off_t)(off + got));
+		if (r < 0 && errno == EINTR) continue;
+		if (r <= 0) break;
+		got += (size_t)r;
+	}
+	return (ssize_t)got;
+}
+
+const uint8_t *find_nl(const uint8_t *p, const uint8_t *e)
+{
+	return p < e ? (const uint8_t *)memchr(p, '\n', (size_t)(e - p)) : nullptr;
+}
+
+// First plausible record header at or after a (a > 0), or -1.  FASTQ: a line
+// "@..." followed by a sequence line, a '+' line and a quality line of the
+// same length, then '@' or end of input.  FASTA: any line starting with '>'
+// or '@' (kseq ends a FASTA record at either).  Only a guess: the caller
+// checks it against the previous piece's end.
+int64_t guess_record(int fd, uint64_t size, uint64_t a, bool fasta, std::vector<uint8_t> &tmp)
+{
+	const uint64_t from = a - 1;
+	const size_t want = (size_t)((size - from) < ((uint64_t)1 << 20) ? (size - from) : ((uint64_t)1 << 20));
+	tmp.resize(want);
+	const ssize_t got = pread_full(fd, tmp.data(), want, from);
+	if (got < 2) return -1;
+	const uint8_t *s = tmp.data(), *e = s + got;
+	const bool at_eof = from + (uint64_t)got >= size;
+	for (const uint8_t *p = s + 1; p < e; ++p) {
+		if (p[-1] != '\n') {
+			p = find_nl(p, e);
+			if (!p) return -1;
+			continue;   // p -> '\n'; the loop steps past it
+		}
+		if (fasta) {
+			if (*p == '>' || *p == '@') return (int64_t)(from + (uint64_t)(p - s));
+			continue;
+		}
+		if (*p != '@') continue;
+		const uint8_t *n1 = find_nl(p, e);
+		const uint8_t *n2 = n1 ? find_nl(n1 + 1, e) : nullptr;
+		if (!n2) return -1;
+		if (n2 + 1 >= e || n2[1] != '+') continue;
+		const uint8_t *n3 = find_nl(n2 + 1, e);
+		if (!n3) return -1;
+		const uint8_t *n4 = find_nl(n3 + 1, e);
+		const uint8_t *qe = n4 ? n4 : (at_eof ? e : nullptr);
+		if (!qe) return -1;
+		if (qe - (n3 + 1) != n2 - (n1 + 1)) continue;
+		if (n4 && n4 + 1 < e && n4[1] != '@') continue;
+		if (n4 && n4 + 1 >= e && !at_eof) return -1;
+		return (int64_t)(from + (uint64_t)(p - s));
+	}
+	return -1;
+}
+
+// Parse records whose header lies in [start, P.b) (kseq semantics from a
+// record boundary) into the piece's slot.
+int parse_piece(int fd, uint64_t size, uint64_t start, int k, int slot, VcIngestSink &sink,
+                VcFastqReader &rd, Piece &P)
+{
+	P.start = (int64_t)start;
+	P.n = P.bytes = 0;
+	P.errs.clear();
+	P.eof = false;
+	P.end = start;
+	if (!rd.open_fd(fd, start, (size_t)1 << 20)) return VC_ENOMEM;
+	size_t used = 0;
+	for (;;) {
+		const int64_t h = rd.peek_header();
+		if (h < 0) {
+			P.eof = true;
+			P.end = size;
+			break;
+		}
+		if ((uint64_t)h >= P.b) {
+			P.end = (uint64_t)h;
+			break;
+		}
+		const int ret = rd.next();
+		if (ret == -1) {
+			P.eof = true;
+			P.end = size;
+			break;
+		}
+		if (ret == -2) {
+			P.errs.push_back(P.n);
+			continue;
+		}
+		if (ret < k) continue;
+		const size_t len = (size_t)ret;
+		if (used + len > P.buf.cap_bytes || P.n + 1 > P.buf.cap_reads) {
+			size_t nb = P.buf.cap_bytes, nr = P.buf.cap_reads;
+			while (used + len > nb) nb = nb * 2 + len;
+			while (P.n + 1 > nr) nr = nr * 2 + 1024;
+			int rc = sink.grow(slot, &P.buf, nb, nr, used, (size_t)P.n);
+			if (rc != VC_OK) return rc;
+		}
+		memcpy(P.buf.seq + used, rd.seq(), len);
+		P.buf.offs[P.n] = used;
+		P.buf.lens[P.n] = (uint32_t)len;
+		used += len;
+		P.bytes += len;
+		++P.n;
+	}
+	return VC_OK;
+}
+
+// The reference's block loop replayed over a piece's accepted reads and -2
+// events (vaf-counter.c:486-517, kthread.c:97-128).  Returns how many of the
+// piece's reads are counted; sets *stopped once the file has ended.
+struct BlockState {
+	int64_t sum = 0;
+	int empty = 0;
+	bool stopped = false;
+};
+
+uint64_t replay_blocks(const Piece &P, int block_bases, BlockState &S, vc_file_stats &st)
+{
+	uint64_t keep = 0;
+	size_t e = 0;
+	auto end_block = [&]() {
+		if (S.sum == 0) {
+			if (++S.empty >= 3) S.stopped = true;
+		} else {
+			++st.blocks;
+		}
+		S.sum = 0;
+	};
+	for (uint64_t i = 0; i <= P.n && !S.stopped; ++i) {
+		while (e < P.errs.size() && P.errs[e] == i && !S.stopped) {
+			end_block();
+			++e;
+		}
+		if (S.stopped || i == P.n) break;
+		const uint32_t len = P.buf.lens[i];
+		S.sum += len;
+		st.bases += len;
+		st.seqs += 1;
+		keep = i + 1;
+		if (S.sum >= block_bases) {
+			++st.blocks;
+			S.sum = 0;
+		}
+	}
+	if (P.eof && !S.stopped) {   // -1 repeats until the third empty block
+		end_block();
+		S.stopped = true;
+	}
+	return keep;
+}
+
+} // namespace
+
+int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, int slots,
+                    uint64_t piece_bytes, VcIngestSink &sink, vc_file_stats &st)
+{
+	if (threads < 1 || slots < threads + 1 || piece_bytes < 2) return VC_EINVAL;
+	if (size == 0) {   // empty input: three empty blocks, nothing counted
+		return VC_OK;
+	}
+	bool fasta = false;
+	{
+		VcFastqReader rd;
+		if (!rd.open_fd(fd, 0, (size_t)1 << 16)) return VC_ENOMEM;
+		const int64_t h = rd.peek_header();
+		if (h < 0) return VC_OK;      // no record at all
+		uint8_t c = 0;
+		if (pread_full(fd, &c, 1, (uint64_t)h) == 1) fasta = c == '>';
+	}
+	const uint64_t np = (size + piece_bytes - 1) / piece_bytes;
+	std::vector<Piece> pcs((size_t)np);
+	std::mutex mu;
+	std::condition_variable cv;
+	uint64_t released = 0;            // pieces whose slot the main thread is done with
+	bool abort = false;
+	std::atomic<uint64_t> next{0};
+
+	auto worker = [&]() {
+		VcFastqReader rd;
+		std::vector<uint8_t> tmp;
+		for (;;) {
+			const uint64_t j = next.fetch_add(1);
+			if (j >= np) return;
+			Piece &P = pcs[(size_t)j];
+			{
+				std::unique_lock<std::mutex> lk(mu);
+				cv.wait(lk, [&] { return abort || j < (uint64_t)slots || released + slots > j; });
+				if (abort) return;
+			}
+			const int slot = (int)(j % (uint64_t)slots);
+			P.a = j * piece_bytes;
+			P.b = P.a + piece_bytes < size ? P.a + piece_bytes : size;
+			int rc = sink.acquire(slot, &P.buf);
+			if (rc == VC_OK) {
+				const int64_t g = j == 0 ? 0 : guess_record(fd, size, P.a, fasta, tmp);
+				if (g >= 0) rc = parse_piece(fd, size, (uint64_t)g, k, slot, sink, rd, P);
+				else P.start = -1;
+			}
+			std::lock_guard<std::mutex> lk(mu);
+			P.rc = rc;
+			P.ready = true;
+			cv.notify_all();
+		}
+	};
+	const int nt = (uint64_t)threads < np ? threads : (int)np;
+	std::vector<std::thread> pool;
+	for (int t = 0; t < nt; ++t) pool.emplace_back(worker);
+
+	int rc = VC_OK;
+	BlockState S;
+	uint64_t expect = 0;              // where the next record's header is
+	VcFastqReader rd;
+	for (uint64_t j = 0; j < np; ++j) {
+		Piece &P = pcs[(size_t)j];
+		{
+			std::unique_lock<std::mutex> lk(mu);
+			cv.wait(lk, [&] { return P.ready; });
+		}
+		const int slot = (int)(j % (uint64_t)slots);
+		if (rc == VC_OK) rc = P.rc;
+		if (rc == VC_OK && !S.stopped && P.b > expect) {
+			if (P.start < 0 || (uint64_t)P.start != expect) // a wrong guess: parse from the true boundary
+				rc = parse_piece(fd, size, expect, k, slot, sink, rd, P);
+			if (rc == VC_OK) {
+				expect = P.end;
+				const uint64_t keep = replay_blocks(P, block_bases, S, st);
+				if (keep) {
+					const uint64_t bytes = (uint64_t)P.buf.offs[keep - 1] + P.buf.lens[keep - 1];
+					rc = sink.submit(slot, P.buf, keep, bytes);
+				}
+			}
+		}
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			released = j + 1;
+			if (rc != VC_OK) abort = true;
+			cv.notify_all();
+		}
+		if (rc != VC_OK) break;   // workers see abort; pieces not yet taken are dropped
+	}
+	for (auto &t : pool) t.join();
+	if (rc == VC_OK && !S.stopped) {
+		// the input ended inside a record the last piece never reached (cannot
+		// happen: the last piece parses to end of input) -- be explicit anyway
+		rc = VC_EINVAL;
+	}
+	return rc;
+}
+
+// ---------------------------------------------------------------------------
+// host-only hook: the parallel ingest without a device (tests, ingest speed)
+// ---------------------------------------------------------------------------
+
+#include <fcntl.h>
+#include <stdlib.h>
+#include <sys/stat.h>
+#include <time.h>
+
+namespace {
+
+class HostSink : public VcIngestSink {
+public:
+	HostSink(int slots, uint64_t piece, uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out, size_t lens_cap)
+		: bufs_((size_t)slots), piece_(piece), seq_out_(seq_out), seq_cap_(seq_cap), lens_out_(lens_out),
+		  lens_cap_(lens_cap) {}
+	~HostSink() override
+	{
+		for (auto &b : bufs_) {
+			free(b.seq);
+			free(b.offs);
+			free(b.lens);
+		}
+	}
+	int acquire(int slot, VcSlotBuf *b) override
+	{
+		VcSlotBuf &s = bufs_[(size_t)slot];
+		if (!s.seq) {
+			int rc = grow(slot, &s, (size_t)piece_ + (size_t)piece_ / 4 + 64, (size_t)piece_ / 64 + 64, 0, 0);
+			if (rc != VC_OK) return rc;
+		}
+		*b = s;
+		return VC_OK;
+	}
+	int grow(int slot, VcSlotBuf *b, size_t bytes, size_t reads, size_t, size_t) override
+	{
+		VcSlotBuf &s = bufs_[(size_t)slot];
+		uint8_t *q = (uint8_t *)realloc(s.seq, bytes);
+		uint64_t *o = (uint64_t *)realloc(s.offs, reads * sizeof(uint64_t));
+		uint32_t *l = (uint32_t *)realloc(s.lens, reads * sizeof(uint32_t));
+		if (q) s.seq = q;
+		if (o) s.offs = o;
+		if (l) s.lens = l;
+		if (!q || !o || !l) return VC_ENOMEM;
+		s.cap_bytes = bytes;
+		s.cap_reads = reads;
+		*b = s;
+		return VC_OK;
+	}
+	int submit(int, const VcSlotBuf &b, uint64_t n, uint64_t bytes) override
+	{
+		if (seq_out_ && nb_ + bytes <= seq_cap_) memcpy(seq_out_ + nb_, b.seq, (size_t)bytes);
+		for (uint64_t i = 0; i < n; ++i)
+			if (lens_out_ && nr_ + i < lens_cap_) lens_out_[nr_ + i] = b.lens[i];
+		nb_ += bytes;
+		nr_ += n;
+		return VC_OK;
+	}
+
+private:
+	std::vector<VcSlotBuf> bufs_;
+	uint64_t piece_;
+	uint8_t *seq_out_;
+	size_t seq_cap_;
+	uint32_t *lens_out_;
+	size_t lens_cap_;
+	uint64_t nb_ = 0, nr_ = 0;
+};
+
+double mono_now()
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+} // namespace
+
+extern "C" int vc_scan_file_parallel(const char *path, int k, int block_bases, int n_threads,
+                                     uint64_t piece_bytes, vc_file_stats *st, uint8_t *seq_out, size_t seq_cap,
+                                     uint32_t *lens_out, size_t lens_cap)
+{
+	if (!path || !st || n_threads < 1 || piece_bytes < 2) return VC_EINVAL;
+	vc_file_stats local = {0, 0, 0, 0.0};
+	const double t0 = mono_now();
+	const int fd = open(path, O_RDONLY);
+	if (fd < 0) return VC_EIO;
+	struct stat sb;
+	if (fstat(fd, &sb) != 0) {
+		close(fd);
+		return VC_EIO;
+	}
+	uint8_t magic[2] = {0, 0};
+	if (pread_full(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b) {
+		close(fd);
+		return VC_EINVAL;   // gzip: sequential reader only
+	}
+	HostSink sink(n_threads + 2, piece_bytes, seq_out, seq_cap, lens_out, lens_cap);
+	const int rc = vc_ingest_plain(fd, (uint64_t)sb.st_size, k, block_bases, n_threads, n_threads + 2,
+	                               piece_bytes, sink, local);
+	close(fd);
+	local.seconds = mono_now() - t0;
+	*st = local;
+	return rc;
+}

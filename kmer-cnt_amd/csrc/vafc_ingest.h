@@ -1,0 +1,63 @@
+// vafc_ingest.h -- parallel ingest of a plain (uncompressed) FASTA/FASTQ file
+// with the reference's exact semantics.
+//
+// The reference reads a file with one kseq stream inside kt_pipeline step 0
+// (vaf-counter.c:486-517, kseq.h:192-232).  Here the file is cut into pieces
+// that worker threads parse concurrently with pread:
+//
+//   * piece j covers the nominal byte range [j P, (j+1) P).  Its worker guesses
+//     the first record header at or after j P (the FASTQ four-line shape, or
+//     a line start with '>'/'@' in FASTA) and parses, with kseq semantics,
+//     every record whose header lies before (j+1) P; the last record may run
+//     past the piece.  It stops at the header of the first record at or past
+//     (j+1) P and reports that offset (`end`).
+//   * the main thread takes the pieces in file order.  A piece whose start
+//     equals the previous piece's end began at a true record boundary in the
+//     same reader state, so its records are exactly the reference's; a piece
+//     wholly inside the previous piece's records is skipped; any other piece
+//     (a wrong guess) is parsed again from the previous end.
+//   * the block loop (blocks of >= -b bases, reads shorter than k skipped, a
+//     -2 from the reader ends a block, the file ends at the third empty
+//     block; vaf-counter.c:486-517, kthread.c:97-128) is replayed over the
+//     accepted reads in order, so a file cut short by empty blocks counts
+//     exactly the reads the reference counts.
+//
+// Accepted reads go straight into the sink's slot buffers (pinned memory for
+// the GPU path); the sink is handed each piece in file order.
+#ifndef VAFC_INGEST_H
+#define VAFC_INGEST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "vafc.h"
+
+struct VcSlotBuf {
+	uint8_t *seq = nullptr;       // accepted reads, concatenated
+	uint64_t *offs = nullptr;
+	uint32_t *lens = nullptr;
+	size_t cap_bytes = 0, cap_reads = 0;
+};
+
+class VcIngestSink {
+public:
+	virtual ~VcIngestSink() = default;
+	// worker thread: slot `slot` may be written (its previous piece has been
+	// consumed); fill *b with its buffers
+	virtual int acquire(int slot, VcSlotBuf *b) = 0;
+	// worker thread: enlarge slot buffers to at least (bytes, reads), keeping
+	// the first `used_bytes` / `used_reads` entries
+	virtual int grow(int slot, VcSlotBuf *b, size_t bytes, size_t reads, size_t used_bytes,
+	                 size_t used_reads) = 0;
+	// main thread, file order: the first n reads (bytes of sequence) of the slot
+	// are accepted
+	virtual int submit(int slot, const VcSlotBuf &b, uint64_t n, uint64_t bytes) = 0;
+};
+
+// Whole-file pass over an open plain file of `size` bytes.  threads >= 1
+// parse workers, `slots` >= threads + 1 slot buffers owned by the sink,
+// pieces of `piece_bytes`.  Fills st (bases, seqs, blocks; not seconds).
+int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, int slots,
+                    uint64_t piece_bytes, VcIngestSink &sink, vc_file_stats &st);
+
+#endif

@@ -36,7 +36,8 @@ EXPORTS = (
     "vc_write_vaf", "vc_pattern_fields", "vc_free", "vc_create", "vc_destroy",
     "vc_count_block", "vc_count_device", "vc_finish", "vc_reset", "vc_device_counts",
     "vc_bind_outputs", "vc_device_tally", "vc_stream", "vc_set_timing", "vc_kernel_ms",
-    "vc_table_info", "vc_count_file", "vc_scan_file", "vc_scan_records", "vc_synth_reads",
+    "vc_table_info", "vc_count_file", "vc_scan_file", "vc_scan_file_parallel", "vc_scan_records",
+    "vc_synth_reads",
     "vc_debug_decode", "vc_strerror", "vc_version",
 )
 
@@ -103,6 +104,8 @@ def lib():
         "vc_count_file": (C.c_int, [P, C.c_char_p, C.c_int, C.c_int, C.POINTER(FileStats)]),
         "vc_scan_file": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(FileStats), P, C.c_size_t,
                                    P, C.c_size_t]),
+        "vc_scan_file_parallel": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_uint64,
+                                            C.POINTER(FileStats), P, C.c_size_t, P, C.c_size_t]),
         "vc_scan_records": (C.c_int64, [C.c_char_p, P, C.c_int64]),
         "vc_synth_reads": (C.c_int, [P, P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
                                      C.c_double, P, P, C.c_uint32, P]),
@@ -317,6 +320,33 @@ def scan_file(fn: str, k: int, block_size: int = 10_000_000, with_reads: bool = 
     if rc == VC_EIO:
         raise FileNotFoundError(fn)
     _ck(rc, "vc_scan_file")
+    return st, reads
+
+
+def scan_file_parallel(fn: str, k: int, block_size: int = 10_000_000, threads: int = 4,
+                       piece_bytes: int = 8 << 20, with_reads: bool = False):
+    """Host-only parallel reader of vc_count_file for plain files (no device):
+    (FileStats, reads or None); the reads are those of scan_file, in order."""
+    st = FileStats()
+    if not with_reads:
+        rc = lib().vc_scan_file_parallel(fn.encode(), k, block_size, threads, piece_bytes, C.byref(st),
+                                         None, 0, None, 0)
+        reads = None
+    else:
+        size = os.path.getsize(fn) + 16
+        seq = np.zeros(max(size, 64), np.uint8)
+        lens = np.zeros(max(size, 16), np.uint32)
+        rc = lib().vc_scan_file_parallel(fn.encode(), k, block_size, threads, piece_bytes, C.byref(st),
+                                         _ptr(seq), seq.size, _ptr(lens), lens.size)
+        reads = []
+        pos = 0
+        for i in range(int(st.seqs)):
+            n = int(lens[i])
+            reads.append(seq[pos:pos + n].tobytes())
+            pos += n
+    if rc == VC_EIO:
+        raise FileNotFoundError(fn)
+    _ck(rc, "vc_scan_file_parallel")
     return st, reads
 
 

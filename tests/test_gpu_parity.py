@@ -283,6 +283,41 @@ def test_count_file_equals_oracle_file_pass(tmp_path):
     assert np.array_equal(got, want[: 2 * orc.n_patterns])
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_count_file_parallel_reader_on_fuzzed_input(seed, tmp_path, monkeypatch):
+    """vc_count_file's parallel reader (forced onto a small file with tiny
+    pieces) on malformed FASTQ/FASTA: counts, bases and k-mers equal the
+    oracle's whole-file pass."""
+    import re
+    import vafc
+    import oracle as O
+    from test_reader import _fuzz_file
+    rng = np.random.default_rng(900 + seed)
+    fq = str(tmp_path / "fuzz.fq")
+    _fuzz_file(fq, rng, 3000)
+    text = open(fq, "rb").read()
+    runs = [m.group(0).decode() for m in re.finditer(rb"[ACGT]{9,}", text)][:60]
+    pat = str(tmp_path / "p.txt")
+    with open(pat, "w") as f:
+        for i, r in enumerate(runs):
+            f.write("chr1\t%d\t%d\trs%d\tA\tC\t%s\t%s\n" % (i, i + 1, i, r[:9], r[1:10]))
+    monkeypatch.setenv("VAFC_INGEST_MIN", "0")
+    monkeypatch.setenv("VAFC_INGEST_PIECE", str(37 + 101 * seed))
+    for b in (10_000_000, 50):
+        db = vafc.load_patterns(pat)
+        m = vafc.create_combined_kmer_map(db, 9)
+        st = m.count_file(fq, b, 3)
+        got, km = m.finish()
+        orc = O.Oracle(9, pattern_fn=pat)
+        want = np.zeros(2 * orc.n_patterns + 2, np.uint32)
+        rc, bases, seqs, km_want = orc.count_file(fq, b, want)
+        assert (st.bases, st.seqs) == (bases, seqs)
+        assert km == km_want
+        assert np.array_equal(got, want[: 2 * orc.n_patterns])
+        assert int(want.sum()) > 0
+        m.close()
+
+
 def test_large_panel_c5_shape():
     """C5 shape: a 200k-SNP panel (~400k keys, saturated LDS prefilter)."""
     import vafc

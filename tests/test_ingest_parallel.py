@@ -1,0 +1,98 @@
+"""The parallel plain-file reader of vc_count_file (vafc_ingest.cpp) against the
+sequential one (vafc_fastq.cpp, pinned to the reference by test_reader.py):
+same accepted reads in the same order, same bases / sequences / blocks, for
+every piece size down to a few bytes (every record boundary is then a piece
+boundary, and most guesses land inside records)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import CASES
+
+from test_reader import READER_FILES, _fuzz_file
+
+PLAIN = [f for f in READER_FILES if not f.endswith(".gz")]
+
+
+def _same(path, k, b, threads, piece):
+    import vafc
+    st0, r0 = vafc.scan_file(path, k, b, with_reads=True)
+    st1, r1 = vafc.scan_file_parallel(path, k, b, threads=threads, piece_bytes=piece, with_reads=True)
+    assert (st1.bases, st1.seqs, st1.blocks) == (st0.bases, st0.seqs, st0.blocks), (path, k, b, threads, piece)
+    assert r1 == r0, (path, k, b, threads, piece)
+
+
+@pytest.mark.parametrize("fn", PLAIN)
+@pytest.mark.parametrize("piece", [2, 7, 64, 1000, 1 << 20])
+def test_golden_reader_files(fn, piece):
+    path = os.path.join(CASES, fn)
+    for k, b in ((1, 10_000_000), (5, 1), (21, 100)):
+        _same(path, k, b, threads=3, piece=piece)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_fuzzed_inputs(seed, tmp_path):
+    """Noise lines, wrapped FASTA, bad quality lengths, CR, '@'/'+' inside
+    records: -2 events end blocks, empty blocks can end a file early."""
+    rng = np.random.default_rng(500 + seed)
+    p = str(tmp_path / "fuzz.fq")
+    _fuzz_file(p, rng, 400)
+    for piece in (3, 17, 111, 4096):
+        for k, b in ((5, 10_000_000), (5, 1), (12, 50), (1, 7)):
+            _same(p, k, b, threads=1 + seed % 5, piece=piece)
+
+
+def _fastq(path, rng, n, L=150, crlf=False):
+    nl = b"\r\n" if crlf else b"\n"
+    with open(path, "wb") as f:
+        for i in range(n):
+            seq = np.frombuffer(b"ACGTN", np.uint8)[rng.integers(0, 5, L)].tobytes()
+            f.write(b"@r%d extra" % i + nl + seq + nl + b"+" + nl + b"I" * L + nl)
+
+
+@pytest.mark.parametrize("crlf", [False, True])
+def test_clean_fastq_many_pieces(tmp_path, crlf):
+    """Well-formed FASTQ: every guess is right, pieces of every size."""
+    rng = np.random.default_rng(7)
+    p = str(tmp_path / "clean.fq")
+    _fastq(p, rng, 5000, crlf=crlf)
+    for piece in (100, 311, 4099, 65536):
+        for threads in (1, 2, 8):
+            _same(p, 21, 10_000, threads, piece)
+
+
+def test_quality_lines_that_look_like_headers(tmp_path):
+    """Quality strings starting with '@' followed by a '+' line: the four-line
+    guess is fooled, the boundary check catches it."""
+    with open(tmp_path / "q.fq", "wb") as f:
+        for i in range(400):
+            s = b"ACGT" * (3 + i % 5)
+            q = b"@" * len(s) if i % 2 else b"+" * len(s)
+            f.write(b"@h%d\n" % i + s + b"\n+\n" + q + b"\n")
+    for piece in (5, 13, 50, 333):
+        _same(str(tmp_path / "q.fq"), 7, 40, 4, piece)
+
+
+def test_fasta_and_long_records(tmp_path):
+    """FASTA (pieces guessed at '>' lines) and records longer than many pieces."""
+    rng = np.random.default_rng(3)
+    with open(tmp_path / "a.fa", "wb") as f:
+        for i in range(60):
+            L = int(rng.integers(1, 5000))
+            s = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, L)].tobytes()
+            f.write(b">c%d\n" % i + b"\n".join(s[j:j + 61] for j in range(0, L, 61)) + b"\n")
+    for piece in (7, 100, 2000, 1 << 20):
+        _same(str(tmp_path / "a.fa"), 15, 3000, 3, piece)
+
+
+def test_gzip_rejected(tmp_path):
+    """The parallel reader is for plain files only (vc_count_file routes gzip
+    to the sequential reader)."""
+    import gzip
+    import vafc
+    p = str(tmp_path / "x.fq.gz")
+    with gzip.open(p, "wb") as f:
+        f.write(b"@a\nACGT\n+\nIIII\n")
+    with pytest.raises(vafc.VafcError):
+        vafc.scan_file_parallel(p, 3)
