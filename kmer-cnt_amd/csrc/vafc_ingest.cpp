@@ -2,7 +2,10 @@
 #include "vafc_ingest.h"
 
 #include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -184,9 +187,20 @@ uint64_t replay_blocks(const Piece &P, int block_bases, BlockState &S, vc_file_s
 
 } // namespace
 
+static double ing_now()
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
 int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, int slots,
                     uint64_t piece_bytes, VcIngestSink &sink, vc_file_stats &st)
 {
+	const bool prof = getenv("VAFC_INGEST_PROFILE") != nullptr;
+	double t_wait = 0, t_submit = 0, t_reparse = 0;
+	std::atomic<uint64_t> t_parse_us{0}, t_slotwait_us{0};
+	const double t_begin = ing_now();
 	if (threads < 1 || slots < threads + 1 || piece_bytes < 2) return VC_EINVAL;
 	if (size == 0) {   // empty input: three empty blocks, nothing counted
 		return VC_OK;
@@ -215,11 +229,13 @@ int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, 
 			const uint64_t j = next.fetch_add(1);
 			if (j >= np) return;
 			Piece &P = pcs[(size_t)j];
+			const double w0 = prof ? ing_now() : 0;
 			{
 				std::unique_lock<std::mutex> lk(mu);
 				cv.wait(lk, [&] { return abort || j < (uint64_t)slots || released + slots > j; });
 				if (abort) return;
 			}
+			const double w1 = prof ? ing_now() : 0;
 			const int slot = (int)(j % (uint64_t)slots);
 			P.a = j * piece_bytes;
 			P.b = P.a + piece_bytes < size ? P.a + piece_bytes : size;
@@ -228,6 +244,11 @@ int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, 
 				const int64_t g = j == 0 ? 0 : guess_record(fd, size, P.a, fasta, tmp);
 				if (g >= 0) rc = parse_piece(fd, size, (uint64_t)g, k, slot, sink, rd, P);
 				else P.start = -1;
+			}
+			if (prof) {
+				const double w2 = ing_now();
+				t_slotwait_us += (uint64_t)((w1 - w0) * 1e6);
+				t_parse_us += (uint64_t)((w2 - w1) * 1e6);
 			}
 			std::lock_guard<std::mutex> lk(mu);
 			P.rc = rc;
@@ -245,21 +266,29 @@ int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, 
 	VcFastqReader rd;
 	for (uint64_t j = 0; j < np; ++j) {
 		Piece &P = pcs[(size_t)j];
+		const double m0 = prof ? ing_now() : 0;
 		{
 			std::unique_lock<std::mutex> lk(mu);
 			cv.wait(lk, [&] { return P.ready; });
 		}
+		const double m1 = prof ? ing_now() : 0;
+		if (prof) t_wait += m1 - m0;
 		const int slot = (int)(j % (uint64_t)slots);
 		if (rc == VC_OK) rc = P.rc;
 		if (rc == VC_OK && !S.stopped && P.b > expect) {
-			if (P.start < 0 || (uint64_t)P.start != expect) // a wrong guess: parse from the true boundary
+			if (P.start < 0 || (uint64_t)P.start != expect) { // a wrong guess: parse from the true boundary
+				const double r0 = prof ? ing_now() : 0;
 				rc = parse_piece(fd, size, expect, k, slot, sink, rd, P);
+				if (prof) t_reparse += ing_now() - r0;
+			}
 			if (rc == VC_OK) {
 				expect = P.end;
 				const uint64_t keep = replay_blocks(P, block_bases, S, st);
 				if (keep) {
 					const uint64_t bytes = (uint64_t)P.buf.offs[keep - 1] + P.buf.lens[keep - 1];
+					const double s0 = prof ? ing_now() : 0;
 					rc = sink.submit(slot, P.buf, keep, bytes);
+					if (prof) t_submit += ing_now() - s0;
 				}
 			}
 		}
@@ -272,6 +301,11 @@ int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, 
 		if (rc != VC_OK) break;   // workers see abort; pieces not yet taken are dropped
 	}
 	for (auto &t : pool) t.join();
+	if (prof)
+		fprintf(stderr, "[ingest] %llu pieces, %d threads: total %.3f s; main: wait %.3f submit %.3f reparse %.3f; "
+		        "workers: parse %.3f slot-wait %.3f (thread-seconds)\n", (unsigned long long)np, threads,
+		        ing_now() - t_begin, t_wait, t_submit, t_reparse, t_parse_us.load() * 1e-6,
+		        t_slotwait_us.load() * 1e-6);
 	if (rc == VC_OK && !S.stopped) {
 		// the input ended inside a record the last piece never reached (cannot
 		// happen: the last piece parses to end of input) -- be explicit anyway

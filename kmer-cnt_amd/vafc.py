@@ -36,7 +36,7 @@ EXPORTS = (
     "vc_write_vaf", "vc_pattern_fields", "vc_free", "vc_create", "vc_destroy",
     "vc_count_block", "vc_count_device", "vc_finish", "vc_reset", "vc_device_counts",
     "vc_bind_outputs", "vc_device_tally", "vc_stream", "vc_set_timing", "vc_kernel_ms",
-    "vc_table_info", "vc_count_file", "vc_scan_file", "vc_scan_file_parallel", "vc_scan_records",
+    "vc_table_info", "vc_count_file", "vc_scan_file", "vc_scan_file_parallel", "vc_scan_records", "vc_reserve_file_ingest",
     "vc_synth_reads",
     "vc_debug_decode", "vc_strerror", "vc_version",
 )
@@ -107,6 +107,7 @@ def lib():
         "vc_scan_file_parallel": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_uint64,
                                             C.POINTER(FileStats), P, C.c_size_t, P, C.c_size_t]),
         "vc_scan_records": (C.c_int64, [C.c_char_p, P, C.c_int64]),
+        "vc_reserve_file_ingest": (C.c_int, [P, C.c_int]),
         "vc_synth_reads": (C.c_int, [P, P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
                                      C.c_double, P, P, C.c_uint32, P]),
         "vc_debug_decode": (C.c_int, [P, C.c_size_t, P, P, C.c_uint64, P, P]),
