@@ -187,6 +187,34 @@ int vc_scan_file_parallel(const char *path, int k, int block_bases, int n_thread
 int64_t vc_scan_records(const char *path, int32_t *rets, int64_t cap);
 
 /* ------------------------------------------------------------------ */
+/* snp-pattern-gen                            */
+/* ------------------------------------------------------------------ */
+
+/* A reference genome in host memory: records, names and sequences exactly
+ * as load_fasta keeps them (snp-pattern-gen.c:67-103: kseq_read until the
+ * first negative return; name = the header up to the first whitespace).
+ * Sequences are stored back to back (vc_fasta_data gives the concatenated
+ * view that vc_count_candidates takes).  Plain or gzip input. */
+typedef struct vc_fasta vc_fasta;
+int vc_fasta_load(const char *path, vc_fasta **out);   /* VC_EIO if unopenable */
+int vc_fasta_count(const vc_fasta *fa);
+const char *vc_fasta_name(const vc_fasta *fa, int i);
+const uint8_t *vc_fasta_seq(const vc_fasta *fa, int i, uint32_t *len);
+int vc_fasta_data(const vc_fasta *fa, const uint8_t **seq, size_t *bytes, const uint64_t **offs,
+                  const uint32_t **lens);
+void vc_fasta_free(vc_fasta *fa);
+
+/* count_candidate_kmers (snp-pattern-gen.c:159-190) on the GPU: counts[i]
+ * (u32, wrapping like the reference's khash values) = the number of
+ * canonical k-mers of all n_seqs sequences that equal keys[i].  Sequences
+ * are decoded with seq_nt4_table at every position (no vaf-counter quirk);
+ * any other byte ends the current window.  keys must be distinct canonical
+ * k-mers; seq/offs/lens are host buffers (sequence i at seq + offs[i]). */
+int vc_count_candidates(int k, const uint8_t *seq, size_t seq_bytes, const uint64_t *offs,
+                        const uint32_t *lens, uint64_t n_seqs, const uint64_t *keys, size_t n_keys,
+                        uint32_t *counts, int device);
+
+/* ------------------------------------------------------------------ */
 /* Synthetic workload (bench / tests): the generator of vafc_synth.py,  */
 /* evaluated on the device.                                            */
 /* ------------------------------------------------------------------ */

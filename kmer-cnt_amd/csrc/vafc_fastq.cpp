@@ -112,6 +112,7 @@ int VcFastqReader::token(int *delim)
 				*delim = c;
 				return 0;
 			}
+			if (keep_name_) name_.push(c);
 		}
 		if (!refill()) return 0;
 	}
@@ -135,7 +136,7 @@ int VcFastqReader::next()
 {
 	int c, d;
 	if (!hdr_ && peek_header() < 0) return -1;   // scan to a '>' or '@' (kseq.h:197-201)
-	seq_.l = qual_.l = 0;
+	seq_.l = qual_.l = name_.l = 0;
 	if (token(&d) < 0) return -1;
 	if (d != '\n' && !at_end()) skip_line();          // comment (kseq.h:204)
 	// sequence lines until a line starts with '+', '>' or '@' (kseq.h:209-213)

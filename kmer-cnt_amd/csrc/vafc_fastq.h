@@ -54,6 +54,10 @@ public:
 	int64_t peek_header();
 	const char *seq() const { return seq_.s; }
 	size_t seq_len() const { return seq_.l; }
+	// keep record names (kseq's name: the header up to the first isspace byte)
+	void keep_names(bool on) { keep_name_ = on; }
+	const char *name() const { return name_.s ? name_.s : ""; }
+	size_t name_len() const { return name_.l; }
 
 private:
 	gzFile fp_ = nullptr;
@@ -65,7 +69,8 @@ private:
 	bool eof_ = false;
 	int hdr_ = 0;                 // header char already consumed, 0 if none
 	uint64_t hdr_pos_ = 0;        // its file offset (pread source)
-	VcByteBuf seq_, qual_;
+	VcByteBuf seq_, qual_, name_;
+	bool keep_name_ = false;
 
 	bool refill();
 	inline int getc_()

@@ -49,6 +49,7 @@ extern "C" {
 #endif
 hipError_t vc_kernel_setup(void);
 hipError_t vc_launch_count(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st);
+hipError_t vc_launch_nt4_normalize(uint8_t *d, uint64_t bytes, hipStream_t st);
 hipError_t vc_launch_decode(const uint8_t *seq, uint64_t seq_bytes, const uint64_t *offs,
                             const uint32_t *lens, uint64_t n_reads, uint8_t *codes, hipStream_t st);
 hipError_t vc_launch_synth(uint8_t *seq, uint64_t *offs, uint32_t *lens, uint64_t first,

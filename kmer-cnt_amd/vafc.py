@@ -37,6 +37,8 @@ EXPORTS = (
     "vc_count_block", "vc_count_device", "vc_finish", "vc_reset", "vc_device_counts",
     "vc_bind_outputs", "vc_device_tally", "vc_stream", "vc_set_timing", "vc_kernel_ms",
     "vc_table_info", "vc_count_file", "vc_scan_file", "vc_scan_file_parallel", "vc_scan_records", "vc_reserve_file_ingest",
+    "vc_fasta_load", "vc_fasta_count", "vc_fasta_name", "vc_fasta_seq", "vc_fasta_data", "vc_fasta_free",
+    "vc_count_candidates",
     "vc_synth_reads",
     "vc_debug_decode", "vc_strerror", "vc_version",
 )
@@ -108,6 +110,14 @@ def lib():
                                             C.POINTER(FileStats), P, C.c_size_t, P, C.c_size_t]),
         "vc_scan_records": (C.c_int64, [C.c_char_p, P, C.c_int64]),
         "vc_reserve_file_ingest": (C.c_int, [P, C.c_int]),
+        "vc_fasta_load": (C.c_int, [C.c_char_p, C.POINTER(P)]),
+        "vc_fasta_count": (C.c_int, [P]),
+        "vc_fasta_name": (C.c_char_p, [P, C.c_int]),
+        "vc_fasta_seq": (P, [P, C.c_int, C.POINTER(C.c_uint32)]),
+        "vc_fasta_data": (C.c_int, [P, C.POINTER(P), C.POINTER(C.c_size_t), C.POINTER(P), C.POINTER(P)]),
+        "vc_fasta_free": (None, [P]),
+        "vc_count_candidates": (C.c_int, [C.c_int, P, C.c_size_t, P, P, C.c_uint64, P, C.c_size_t, P,
+                                          C.c_int]),
         "vc_synth_reads": (C.c_int, [P, P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
                                      C.c_double, P, P, C.c_uint32, P]),
         "vc_debug_decode": (C.c_int, [P, C.c_size_t, P, P, C.c_uint64, P, P]),
@@ -480,3 +490,43 @@ def main(argv=None) -> int:
 
 if __name__ == "__main__":
     sys.exit(main())
+
+
+# --------------------------------------------------------------------------
+# snp-pattern-gen
+# --------------------------------------------------------------------------
+
+def load_fasta(fn: str):
+    """load_fasta (snp-pattern-gen.c:67-103): [(name, sequence bytes)]."""
+    h = P()
+    rc = lib().vc_fasta_load(fn.encode(), C.byref(h))
+    if rc == VC_EIO:
+        raise FileNotFoundError(fn)
+    _ck(rc, "vc_fasta_load")
+    try:
+        out = []
+        for i in range(lib().vc_fasta_count(h)):
+            n = C.c_uint32()
+            p = lib().vc_fasta_seq(h, i, C.byref(n))
+            out.append((lib().vc_fasta_name(h, i), C.string_at(p, n.value) if n.value else b""))
+        return out
+    finally:
+        lib().vc_fasta_free(h)
+
+
+def count_candidate_kmers(k: int, seqs, keys, device: int = 0) -> np.ndarray:
+    """count_candidate_kmers (snp-pattern-gen.c:159-190) on the GPU: for each of
+    the distinct canonical keys, how often it occurs among the canonical
+    k-mers of the sequences (u32)."""
+    seqs = [bytes(s) for s in seqs]
+    blob = np.frombuffer(b"".join(seqs), np.uint8) if any(seqs) else np.zeros(1, np.uint8)
+    lens = np.array([len(s) for s in seqs], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)[:-1]]).astype(np.uint64) if len(seqs) else \
+        np.zeros(1, np.uint64)
+    keys = np.ascontiguousarray(keys, np.uint64)
+    counts = np.zeros(max(keys.size, 1), np.uint32)
+    blob = np.ascontiguousarray(blob)
+    _ck(lib().vc_count_candidates(k, _ptr(blob), int(sum(len(s) for s in seqs)), _ptr(offs), _ptr(lens),
+                                  len(seqs), _ptr(keys), keys.size, _ptr(counts), device),
+        "vc_count_candidates")
+    return counts[:keys.size]

@@ -42,6 +42,8 @@ def lib():
         L.orc_count_file.argtypes = [P, C.c_char_p, C.c_int, P, P, P, P]
         L.orc_scan_records.restype = C.c_int64
         L.orc_scan_records.argtypes = [C.c_char_p, P, C.c_int64]
+        L.orc_fasta_records.restype = C.c_int64
+        L.orc_fasta_records.argtypes = [C.c_char_p, P, C.c_size_t, P, C.c_int64, P, C.c_size_t]
         _lib = L
     return _lib
 
@@ -125,3 +127,26 @@ def scan_records(fn, cap=1 << 20):
     if n < 0:
         raise FileNotFoundError(fn)
     return rets[:min(n, cap)]
+
+
+def fasta_records(fn):
+    """[(name, seq)] of every record until the first kseq_read < 0 (the loop of
+    snp-pattern-gen's load_fasta, snp-pattern-gen.c:82-98)."""
+    import gzip
+    raw = open(fn, "rb").read()
+    if raw[:2] == b"\x1f\x8b":
+        raw = gzip.decompress(raw)
+    cap = len(raw) + 16
+    seq = np.zeros(cap, np.uint8)
+    lens = np.zeros(cap, np.uint32)
+    names = np.zeros(cap, np.uint8)
+    n = lib().orc_fasta_records(fn.encode(), _p(seq), cap, _p(lens), cap, _p(names), cap)
+    if n < 0:
+        raise FileNotFoundError(fn)
+    out, pos = [], 0
+    nm = names.tobytes().split(b"\0")
+    for i in range(n):
+        L = int(lens[i])
+        out.append((nm[i], seq[pos:pos + L].tobytes()))
+        pos += L
+    return out
