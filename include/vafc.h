@@ -204,6 +204,11 @@ int vc_fasta_data(const vc_fasta *fa, const uint8_t **seq, size_t *bytes, const 
                   const uint32_t **lens);
 void vc_fasta_free(vc_fasta *fa);
 
+/* Decode mode of a counter: on = seq_nt4_table at every position, the decode
+ * of snp-pattern-gen (snp-pattern-gen.c:165), instead of vaf-counter's
+ * position-dependent one (the default).  Applies to later count calls. */
+int vc_set_nt4_decode(vc_ctx *ctx, int on);
+
 /* count_candidate_kmers (snp-pattern-gen.c:159-190) on the GPU: counts[i]
  * (u32, wrapping like the reference's khash values) = the number of
  * canonical k-mers of all n_seqs sequences that equal keys[i].  Sequences

@@ -235,6 +235,7 @@ struct vc_ctx {
 	int n_cu = 256;
 	vc_slot_t *d_table = nullptr;
 	int ablate = 0;                   // kernel ablation variant (libvafc_abl.so only)
+	int nt4 = 0;                      // seq_nt4 decode everywhere (vc_set_nt4_decode)
 	uint32_t tbits = 0;
 	uint32_t *d_filter = nullptr;
 	uint32_t wbits = 0;
@@ -448,6 +449,7 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 	A.l2f = c->d_l2f;
 	A.l2bits = c->l2bits;
 	A.ablate = c->ablate;
+	A.nt4 = (uint32_t)c->nt4;
 	A.k = c->k;
 	A.kmask = ((uint64_t)1 << (2 * c->k)) - 1;
 	A.counts = c->d_counts;
@@ -465,6 +467,13 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 		HIPCK(hipEventRecord(c->t1, st));
 		c->timed = true;
 	}
+	return VC_OK;
+}
+
+extern "C" int vc_set_nt4_decode(vc_ctx *c, int on)
+{
+	if (!c) return VC_EINVAL;
+	c->nt4 = on ? 1 : 0;
 	return VC_OK;
 }
 

@@ -28,6 +28,7 @@ struct VcKernelArgs {
 	const uint32_t *l2f;         // second-level filter (vc_l2f_*), NULL = off
 	uint32_t l2bits;
 	int ablate;                  // ablation builds only (VAFC_ABLATE), 0 otherwise
+	uint32_t nt4;                // 1: seq_nt4_table decode everywhere (snp-pattern-gen), 0: vaf-counter
 	int k;
 	uint64_t kmask;              // (1 << 2k) - 1
 	uint32_t *counts;            // [2 * n_patterns]
@@ -49,7 +50,6 @@ extern "C" {
 #endif
 hipError_t vc_kernel_setup(void);
 hipError_t vc_launch_count(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st);
-hipError_t vc_launch_nt4_normalize(uint8_t *d, uint64_t bytes, hipStream_t st);
 hipError_t vc_launch_decode(const uint8_t *seq, uint64_t seq_bytes, const uint64_t *offs,
                             const uint32_t *lens, uint64_t n_reads, uint8_t *codes, hipStream_t st);
 hipError_t vc_launch_synth(uint8_t *seq, uint64_t *offs, uint32_t *lens, uint64_t first,

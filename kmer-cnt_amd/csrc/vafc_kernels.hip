@@ -13,42 +13,6 @@ VC_K_LIST(VC_K_DECL)
 #undef VC_K_DECL
 
 // ---------------------------------------------------------------------------
-// seq_nt4 normaliser (snp-pattern-gen): every byte becomes the letter of its
-// seq_nt4_table code ("ACGT", 'N' for 4).  The counting kernels decode the
-// first 16 floor(len/16) bytes of a sequence with the vaf-counter quirk
-// (vaf-counter.c:261-291); on normalised bytes both decodes agree, so the same
-// kernels count with snp-pattern-gen's plain seq_nt4_table decode
-// (snp-pattern-gen.c:165).  HBM-bound: 16 B per lane, grid-stride.
-// ---------------------------------------------------------------------------
-
-__global__ void __launch_bounds__(256) vc_nt4_normalize_kernel(uint32_t *w, uint64_t n_quads)
-{
-	const uint32_t TBL_LO = 0x54474341u;   // 'A' 'C' 'G' 'T'
-	const uint32_t TBL_HI = 0x4E4E4E4Eu;   // 'N' x 4 (codes with the invalid bit)
-	for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n_quads;
-	     q += (uint64_t)gridDim.x * blockDim.x) {
-		uint4 v = reinterpret_cast<uint4 *>(w)[q];
-		v.x = __builtin_amdgcn_perm(TBL_HI, TBL_LO, dec_tail(v.x) & 0x07070707u);
-		v.y = __builtin_amdgcn_perm(TBL_HI, TBL_LO, dec_tail(v.y) & 0x07070707u);
-		v.z = __builtin_amdgcn_perm(TBL_HI, TBL_LO, dec_tail(v.z) & 0x07070707u);
-		v.w = __builtin_amdgcn_perm(TBL_HI, TBL_LO, dec_tail(v.w) & 0x07070707u);
-		reinterpret_cast<uint4 *>(w)[q] = v;
-	}
-}
-
-extern "C" hipError_t vc_launch_nt4_normalize(uint8_t *d, uint64_t bytes, hipStream_t st)
-{
-	// d is 16-byte aligned and padded to a multiple of 16 bytes by the caller
-	const uint64_t nq = (bytes + 15) / 16;
-	if (nq == 0) return hipSuccess;
-	uint64_t blocks = (nq + 255) / 256;
-	if (blocks > 8192) blocks = 8192;
-	hipLaunchKernelGGL(vc_nt4_normalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
-	                   reinterpret_cast<uint32_t *>(d), nq);
-	return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
 // debug kernel: position-dependent decode of whole reads (tests only)
 // ---------------------------------------------------------------------------
 

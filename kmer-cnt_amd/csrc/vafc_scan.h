@@ -364,7 +364,12 @@ __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t 
 {
 	const uint32_t fsh = A.fsh;
 	const uint32_t zero_word = 1u << A.wbits;   // an all-zero LDS word past the filter
-	const int tail_c = (len & 15) ? (len >> 4) : -1;
+	// the read's tail chunk decodes with seq_nt4_table (vaf-counter.c:261-291);
+	// in seq_nt4 mode (snp-pattern-gen) every chunk does: tail_c = -1 and the
+	// test (c | -1) == -1 always holds (the OR is scalar in the reads kernel)
+	const int tail_c = A.nt4 ? -1 : ((len & 15) ? (len >> 4) : -1);
+	const int nt4m = -(int)A.nt4;   // 0 or -1 (the host stores 0 / 1); kept arithmetic so
+	                                  // the test stays one compare, not (c == tail_c) || nt4
 
 	uint64_t addr = off + 16ull * (uint64_t)c_lo;
 	uint64_t wi = addr >> 2;
@@ -395,8 +400,9 @@ __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t 
 		const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
 		const uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
 		uint32_t t0 = dec_head(b0), t1 = dec_head(b1), t2 = dec_head(b2), t3 = dec_head(b3);
-		if (__ballot(c == tail_c)) {
-			if (c == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
+		const int cm = c | nt4m;
+		if (__ballot(cm == tail_c)) {
+			if (cm == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
 		}
 		const int P = 16 * c;
 		if (__ballot(P + 16 > vhi)) {   // past the span end (and inactive lanes: P >= vhi)
@@ -491,7 +497,7 @@ __device__ __forceinline__ int clamp16(int v) { return v < 0 ? 0 : (v > 16 ? 16 
 // holding the chunk's first byte, realigned by sh); (B1, C1) / (B2, C2) are
 // the streams of chunks c-1 / c-2 and move on to c / c-1.
 template <int K, int ABL>
-__device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int tail_c, uint32_t sh,
+__device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int tail_c, int nt4m, uint32_t sh,
                                              uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
                                              uint32_t &Bm1, uint32_t &Bm2, uint32_t &Cm1, uint32_t &Cm2,
                                              int &U, int &Qe, const uint32_t *__restrict__ filt, WaveQueue &Q,
@@ -506,8 +512,9 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 	const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
 	const uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
 	uint32_t t0 = dec_head(b0), t1 = dec_head(b1), t2 = dec_head(b2), t3 = dec_head(b3);
-	if (__ballot(c == tail_c)) {
-		if (c == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
+	const int cm = c | nt4m;
+	if (__ballot(cm == tail_c)) {
+		if (cm == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
 	}
 	U += 16;
 	Qe += 16;
@@ -636,7 +643,12 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
                                                  uint32_t &tl, int lane)
 {
 	static_assert(K >= 16 && K <= 31, "packed scan needs 16 <= k <= 31");
-	const int tail_c = (len & 15) ? (len >> 4) : -1;
+	// the read's tail chunk decodes with seq_nt4_table (vaf-counter.c:261-291);
+	// in seq_nt4 mode (snp-pattern-gen) every chunk does: tail_c = -1 and the
+	// test (c | -1) == -1 always holds (the OR is scalar in the reads kernel)
+	const int tail_c = A.nt4 ? -1 : ((len & 15) ? (len >> 4) : -1);
+	const int nt4m = -(int)A.nt4;   // 0 or -1 (the host stores 0 / 1); kept arithmetic so
+	                                  // the test stays one compare, not (c == tail_c) || nt4
 
 	uint64_t addr = off + 16ull * (uint64_t)c_lo;
 	uint64_t wi = addr >> 2;
@@ -682,8 +694,8 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 		}
 		quad_fix(d1, w1, w2, w3, w4);
 		quad_fix(d5, w5, w6, w7, w8);
-		packed_chunk<K, ABL>(A, c, tail_c, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
-		packed_chunk<K, ABL>(A, c + 1, tail_c, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
+		packed_chunk<K, ABL>(A, c, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
+		packed_chunk<K, ABL>(A, c + 1, tail_c, nt4m, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
 		w0 = w8;
 		w1 = n0; w2 = n1; w3 = n2; w4 = n3; d1 = dn0;
 		w5 = n4; w6 = n5; w7 = n6; w8 = n7; d5 = dn4;
@@ -694,9 +706,9 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 		const int c = c_lo + it;
 		quad_fix(d1, w1, w2, w3, w4);
 		quad_fix(d5, w5, w6, w7, w8);
-		packed_chunk<K, ABL>(A, c, tail_c, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
+		packed_chunk<K, ABL>(A, c, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
 		if (it + 1 < nit)
-			packed_chunk<K, ABL>(A, c + 1, tail_c, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl,
+			packed_chunk<K, ABL>(A, c + 1, tail_c, nt4m, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl,
 			                     lane);
 	}
 }

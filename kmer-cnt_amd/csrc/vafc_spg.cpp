@@ -5,9 +5,9 @@
 // canonical k-mers that are candidate keys (the ref and alt k-mers of the
 // BED's SNPs) -- count_candidate_kmers, snp-pattern-gen.c:159-190.  That is
 // the vaf-counter scan with a different decode and one counter per key:
-//   * the genome is copied to HBM and normalised in place (every byte becomes
-//     the letter of its seq_nt4_table code), after which the counting kernels'
-//     position-dependent decode equals snp-pattern-gen's plain one;
+//   * the genome is copied to HBM and counted in seq_nt4 mode
+//     (vc_set_nt4_decode): every chunk takes the exact seq_nt4_table decode
+//     that vaf-counter's kernels use only for a read's tail;
 //   * the candidate keys become a key table whose value is the key's own
 //     index, so counts[i] is the number of occurrences of keys[i];
 //   * chromosomes (longer than 16,384 bases) take the segmented long-read
@@ -111,20 +111,17 @@ extern "C" int vc_count_candidates(int k, const uint8_t *seq, size_t seq_bytes, 
 	vc_ctx *ctx = nullptr;
 	int rc = vc_create(&ctx, k, keys, vals.data(), n_keys, n_patterns, device);
 	if (rc != VC_OK) return rc;
+	vc_set_nt4_decode(ctx, 1);
 	uint8_t *d_seq = nullptr;
 	uint64_t *d_offs = nullptr;
 	uint32_t *d_lens = nullptr;
-	const size_t padded = (seq_bytes + 15) / 16 * 16 + 16;
 	if (n_seqs) {
-		SPGCK(hipMalloc(&d_seq, padded));
-		SPGCK(hipMemset(d_seq, 'N', padded));
+		SPGCK(hipMalloc(&d_seq, seq_bytes + 16));
 		SPGCK(hipMemcpy(d_seq, seq, seq_bytes, hipMemcpyHostToDevice));
 		SPGCK(hipMalloc(&d_offs, n_seqs * sizeof(uint64_t)));
 		SPGCK(hipMalloc(&d_lens, n_seqs * sizeof(uint32_t)));
 		SPGCK(hipMemcpy(d_offs, offs, n_seqs * sizeof(uint64_t), hipMemcpyHostToDevice));
 		SPGCK(hipMemcpy(d_lens, lens, n_seqs * sizeof(uint32_t), hipMemcpyHostToDevice));
-		SPGCK(vc_launch_nt4_normalize(d_seq, padded, nullptr));
-		SPGCK(hipDeviceSynchronize());
 		rc = vc_count_device(ctx, d_seq, seq_bytes, d_offs, d_lens, n_seqs, nullptr);
 		if (rc != VC_OK) goto done;
 	}

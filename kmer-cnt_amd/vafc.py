@@ -38,7 +38,7 @@ EXPORTS = (
     "vc_bind_outputs", "vc_device_tally", "vc_stream", "vc_set_timing", "vc_kernel_ms",
     "vc_table_info", "vc_count_file", "vc_scan_file", "vc_scan_file_parallel", "vc_scan_records", "vc_reserve_file_ingest",
     "vc_fasta_load", "vc_fasta_count", "vc_fasta_name", "vc_fasta_seq", "vc_fasta_data", "vc_fasta_free",
-    "vc_count_candidates",
+    "vc_count_candidates", "vc_set_nt4_decode",
     "vc_synth_reads",
     "vc_debug_decode", "vc_strerror", "vc_version",
 )
@@ -116,6 +116,7 @@ def lib():
         "vc_fasta_seq": (P, [P, C.c_int, C.POINTER(C.c_uint32)]),
         "vc_fasta_data": (C.c_int, [P, C.POINTER(P), C.POINTER(C.c_size_t), C.POINTER(P), C.POINTER(P)]),
         "vc_fasta_free": (None, [P]),
+        "vc_set_nt4_decode": (C.c_int, [P, C.c_int]),
         "vc_count_candidates": (C.c_int, [C.c_int, P, C.c_size_t, P, P, C.c_uint64, P, C.c_size_t, P,
                                           C.c_int]),
         "vc_synth_reads": (C.c_int, [P, P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
@@ -124,7 +125,10 @@ def lib():
         "vc_strerror": (C.c_char_p, [C.c_int]),
         "vc_version": (C.c_int, []),
     }
+    older = "VAFC_LIB" in os.environ      # A/B against an older build: bind what it has
     for name, (res, args) in sig.items():
+        if older and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
