@@ -154,8 +154,9 @@ typedef struct {
  * at the third empty block (vaf-counter.c:486-517, kthread.c:97-128).  Reads
  * are streamed to the device in large pinned batches.  Plain (uncompressed)
  * files of 32 MB or more are parsed by n_threads worker threads (the CLI's
- * -t; vafc_ingest.h) with identical results; gzip and small files use one
- * reader thread.  Returns VC_EIO if the file cannot be opened (the reference
+ * -t; vafc_ingest.h) with identical results; gzip files are inflated by
+ * n_threads workers (vafc_gzip.h, gzread's output) and parsed by one thread;
+ * small plain files use one reader thread.  Returns VC_EIO if the file cannot be opened (the reference
  * skips such files silently, vaf-counter.c:557). */
 int vc_count_file(vc_ctx *ctx, const char *path, int block_bases, int n_threads,
                   vc_file_stats *st);
@@ -177,10 +178,22 @@ int vc_scan_file(const char *path, int k, int block_bases, vc_file_stats *st,
  * without a device: n_threads workers parse pieces of piece_bytes of the file
  * concurrently (vafc_ingest.h); accepted reads come out in file order, exactly
  * as vc_scan_file's.  Lets the parallel reader be checked without a GPU and
- * measures its speed.  gzip input is rejected (VC_EINVAL). */
+ * measures its speed.  gzip input: n_threads inflate workers with chunks of
+ * piece_bytes compressed bytes (the reader of vc_count_file for .gz), the
+ * block loop in the calling thread. */
 int vc_scan_file_parallel(const char *path, int k, int block_bases, int n_threads, uint64_t piece_bytes,
                           vc_file_stats *st, uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out,
                           size_t lens_cap);
+
+/* Host-only gzip inflate (test and speed hooks): the whole decompressed
+ * stream of `path` -- through the parallel inflater (n_threads workers,
+ * chunk_bytes compressed bytes per chunk; stats6 = chunks, accepted, skipped,
+ * zlib fallbacks, members checked, CRC error) or through zlib's gzread --
+ * written to out while it fits.  Returns the stream's length, or -1 if the
+ * file cannot be opened (parallel: is not gzip). */
+int64_t vc_gz_inflate_parallel(const char *path, int n_threads, uint64_t chunk_bytes, uint8_t *out,
+                               uint64_t cap, uint64_t *stats6);
+int64_t vc_gz_inflate_zlib(const char *path, uint8_t *out, uint64_t cap);
 
 /* Host-only: the kseq_read return value of every record until -1 (inclusive),
  * written while they fit; returns the number of calls made, or VC_EIO. */
@@ -196,7 +209,8 @@ int64_t vc_scan_records(const char *path, int32_t *rets, int64_t cap);
  * Sequences are stored back to back (vc_fasta_data gives the concatenated
  * view that vc_count_candidates takes).  Plain or gzip input. */
 typedef struct vc_fasta vc_fasta;
-int vc_fasta_load(const char *path, vc_fasta **out);   /* VC_EIO if unopenable */
+int vc_fasta_load(const char *path, vc_fasta **out);   /* VC_EIO if unopenable; gzip inflated
+                                                          by up to 16 threads (VAFC_THREADS) */
 int vc_fasta_count(const vc_fasta *fa);
 const char *vc_fasta_name(const vc_fasta *fa, int i);
 const uint8_t *vc_fasta_seq(const vc_fasta *fa, int i, uint32_t *len);

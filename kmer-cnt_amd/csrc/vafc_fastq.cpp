@@ -1,5 +1,6 @@
 // vafc_fastq.cpp -- see vafc_fastq.h.
 #include "vafc_fastq.h"
+#include "vafc_gzip.h"
 
 #include <ctype.h>
 #include <stdlib.h>
@@ -12,6 +13,31 @@ bool VcFastqReader::open(const char *path, size_t window)
 	fp_ = gzopen(path, "r");
 	if (!fp_) return false;
 	gzbuffer(fp_, 1u << 20);
+	cap_ = window;
+	buf_ = (uint8_t *)malloc(cap_);
+	b_ = e_ = 0;
+	eof_ = false;
+	hdr_ = 0;
+	return buf_ != nullptr;
+}
+
+// Compressed bytes per inflate chunk of the parallel gzip reader (about
+// 14 MB of FASTQ text at level 6).
+#ifndef VC_GZ_CHUNK_BYTES
+#define VC_GZ_CHUNK_BYTES ((uint64_t)4 << 20)
+#endif
+
+bool VcFastqReader::open_parallel(const char *path, int threads, uint64_t chunk_bytes, size_t window)
+{
+	close();
+	if (threads >= 1) {
+		if (!chunk_bytes) {
+			const char *e = getenv("VAFC_GZ_CHUNK");   // test knob
+			chunk_bytes = e && atoll(e) > 0 ? (uint64_t)atoll(e) : VC_GZ_CHUNK_BYTES;
+		}
+		gzp_ = vc_gzp_open(path, threads, chunk_bytes);
+	}
+	if (!gzp_) return open(path, window);
 	cap_ = window;
 	buf_ = (uint8_t *)malloc(cap_);
 	b_ = e_ = 0;
@@ -37,6 +63,8 @@ void VcFastqReader::close()
 {
 	if (fp_) gzclose(fp_);
 	fp_ = nullptr;
+	if (gzp_) vc_gzp_close(gzp_);
+	gzp_ = nullptr;
 	fd_ = -1;
 	free(buf_);
 	buf_ = nullptr;
@@ -50,6 +78,8 @@ bool VcFastqReader::refill()
 		do n = pread(fd_, buf_, cap_, (off_t)foff_); while (n < 0 && errno == EINTR);
 		base_ = foff_;
 		if (n > 0) foff_ += (uint64_t)n;
+	} else if (gzp_) {
+		n = (ssize_t)vc_gzp_read(gzp_, buf_, cap_);
 	} else {
 		n = gzread(fp_, buf_, (unsigned)cap_);
 	}

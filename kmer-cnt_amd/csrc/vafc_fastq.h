@@ -15,6 +15,8 @@
 #include <string.h>
 #include <zlib.h>
 
+class VcGzParallel;
+
 class VcByteBuf {
 public:
 	char *s = nullptr;
@@ -42,6 +44,12 @@ public:
 	VcFastqReader() = default;
 	~VcFastqReader() { close(); }
 	bool open(const char *path, size_t window = (size_t)4 << 20);
+	// As open(), but a gzip file is inflated by `threads` workers
+	// (vafc_gzip.h) with gzread's output; plain files and gzip files the
+	// parallel inflater declines are read as open() reads them.
+	bool open_parallel(const char *path, int threads, uint64_t chunk_bytes = 0,
+	                   size_t window = (size_t)4 << 20);
+	bool gz_parallel() const { return gzp_ != nullptr; }
 	// Plain-file source for the parallel ingest: records from file offset
 	// `off` of an open descriptor (read with pread, the descriptor is not
 	// owned).  `off` must be where kseq would look for a record's header.
@@ -61,6 +69,7 @@ public:
 
 private:
 	gzFile fp_ = nullptr;
+	VcGzParallel *gzp_ = nullptr;   // parallel gzip source (open_parallel)
 	int fd_ = -1;                 // pread source (open_fd), not owned
 	uint64_t foff_ = 0;           // file offset of the next pread
 	uint64_t base_ = 0;           // file offset of buf_[0] (pread source)

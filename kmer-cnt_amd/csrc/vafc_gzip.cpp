@@ -1,0 +1,1106 @@
+// vafc_gzip.cpp -- see vafc_gzip.h.
+//
+// Deflate (RFC 1951) and gzip (RFC 1952) are restated here from the formats;
+// zlib (the reference's gzread, pinned by the system package) remains the
+// decoder of record for every chunk whose speculative decode is not used.
+#include "vafc_gzip.h"
+
+#include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <time.h>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace {
+
+double gz_now()
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+std::atomic<uint64_t> prof_search_us{0}, prof_decode_us{0}, prof_resolve_us{0}, prof_crc_us{0};
+
+constexpr uint32_t WSIZE = 32768;             // deflate history
+constexpr uint16_t MARK = 0x8000;             // symbol = MARK | window index
+constexpr size_t OUT_CAP = (size_t)64 << 20;  // symbols per speculative chunk
+constexpr size_t PIECE_CAP = (size_t)16 << 20;  // bytes per zlib-fallback piece
+
+inline uint32_t le32(const uint8_t *p) { return p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24; }
+
+// ---------------------------------------------------------------------------
+// bit input: LSB-first, 64-bit buffer refilled with whole unaligned words
+// (the bits above `cnt` are always either zero or the true next bits)
+// ---------------------------------------------------------------------------
+struct BitIn {
+	const uint8_t *p = nullptr;
+	uint64_t n = 0;       // input bytes
+	uint64_t pos = 0;     // next byte to load
+	uint64_t buf = 0;
+	unsigned cnt = 0;     // valid bits in buf
+
+	void init(const uint8_t *p_, uint64_t n_, uint64_t bitoff)
+	{
+		p = p_;
+		n = n_;
+		pos = bitoff >> 3;
+		buf = 0;
+		cnt = 0;
+		refill();
+		drop((unsigned)(bitoff & 7));
+	}
+	inline void refill()
+	{
+		if (__builtin_expect(pos + 8 <= n, 1)) {
+			uint64_t w;
+			memcpy(&w, p + pos, 8);
+			buf |= w << cnt;
+			pos += (63 - cnt) >> 3;
+			cnt |= 56;
+		} else {
+			while (cnt <= 56) {
+				const uint64_t b = pos < n ? p[pos] : 0;
+				buf |= b << cnt;
+				++pos;
+				cnt += 8;
+			}
+		}
+	}
+	inline uint64_t bitpos() const { return pos * 8 - cnt; }
+	inline bool overrun() const { return bitpos() > n * 8; }
+	inline void drop(unsigned k)
+	{
+		buf >>= k;
+		cnt -= k;
+	}
+	inline uint32_t take(unsigned k)
+	{
+		const uint32_t v = (uint32_t)(buf & ((1ull << k) - 1));
+		drop(k);
+		return v;
+	}
+};
+
+// ---------------------------------------------------------------------------
+// Huffman decoding tables.  Entry: bits 0-7 code length to consume, 8-12 extra
+// bits (or sub-table index bits), 13-15 kind, 16-31 value.
+// ---------------------------------------------------------------------------
+enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_SUB = 3, K_BAD = 4 };
+inline uint32_t mk(uint32_t len, uint32_t ext, uint32_t kind, uint32_t val)
+{
+	return len | ext << 8 | kind << 13 | val << 16;
+}
+inline uint32_t e_len(uint32_t e) { return e & 0xff; }
+inline uint32_t e_ext(uint32_t e) { return (e >> 8) & 31; }
+inline uint32_t e_kind(uint32_t e) { return (e >> 13) & 7; }
+inline uint32_t e_val(uint32_t e) { return e >> 16; }
+
+const uint16_t LBASE[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115,
+                            131, 163, 195, 227, 258};
+const uint8_t LEXT[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+const uint16_t DBASE[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769, 1025,
+                            1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+const uint8_t DEXT[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12,
+                          13, 13};
+const uint8_t CL_ORDER[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+constexpr unsigned LROOT = 11, DROOT = 8, CROOT = 7;
+constexpr size_t LTAB = (1u << LROOT) + 288 * 16;
+constexpr size_t DTAB = (1u << DROOT) + 32 * 128;
+
+enum Code { C_CL, C_LIT, C_DIST };
+
+inline uint32_t sym_entry(Code c, unsigned s, unsigned len)
+{
+	if (c == C_LIT) {
+		if (s < 256) return mk(len, 0, K_LIT, s);
+		if (s == 256) return mk(len, 0, K_EOB, 0);
+		if (s <= 285) return mk(len, LEXT[s - 257], K_LEN, LBASE[s - 257]);
+		return mk(len, 0, K_BAD, 0);
+	}
+	if (c == C_DIST) return s < 30 ? mk(len, DEXT[s], K_LIT, DBASE[s]) : mk(len, 0, K_BAD, 0);
+	return mk(len, 0, K_LIT, s);
+}
+
+inline unsigned rev(unsigned x, unsigned n)
+{
+	unsigned r = 0;
+	for (unsigned i = 0; i < n; ++i) r |= ((x >> i) & 1) << (n - 1 - i);
+	return r;
+}
+
+// zlib's acceptance rules (inflate_table): over-subscribed codes are errors;
+// an incomplete code-length code is an error; an incomplete literal/length or
+// distance code is accepted only when its longest code has length 1; a code
+// with no symbols at all is accepted (decoding from it is the error).
+bool build(uint32_t *T, unsigned root, const uint8_t *lens, unsigned n, Code c)
+{
+	unsigned count[16] = {0};
+	for (unsigned i = 0; i < n; ++i) count[lens[i]]++;
+	count[0] = 0;
+	unsigned maxlen = 15;
+	while (maxlen && !count[maxlen]) --maxlen;
+	const uint32_t bad = mk(1, 0, K_BAD, 0);
+	for (unsigned i = 0; i < (1u << root); ++i) T[i] = bad;
+	if (maxlen == 0) return c != C_CL;
+	int left = 1;
+	for (unsigned l = 1; l <= 15; ++l) {
+		left <<= 1;
+		left -= (int)count[l];
+		if (left < 0) return false;
+	}
+	if (left > 0 && (c == C_CL || maxlen != 1)) return false;
+	unsigned offs[16];
+	offs[1] = 0;
+	for (unsigned l = 1; l < 15; ++l) offs[l + 1] = offs[l] + count[l];
+	uint16_t sorted[320];
+	for (unsigned s = 0; s < n; ++s)
+		if (lens[s]) sorted[offs[lens[s]]++] = (uint16_t)s;
+	unsigned code = 0, idx = 0;
+	const unsigned short_max = maxlen < root ? maxlen : root;
+	for (unsigned l = 1; l <= short_max; ++l) {
+		for (unsigned c2 = 0; c2 < count[l]; ++c2) {
+			const unsigned s = sorted[idx++];
+			const uint32_t e = sym_entry(c, s, l);
+			for (unsigned k = rev(code, l); k < (1u << root); k += 1u << l) T[k] = e;
+			++code;
+		}
+		code <<= 1;
+	}
+	if (maxlen <= root) return true;
+	// longer codes: one sub-table per root prefix, sized for its longest code
+	uint8_t ml[1u << LROOT];
+	{
+		unsigned cc = code;
+		for (unsigned l = root + 1; l <= maxlen; ++l) {
+			for (unsigned c2 = 0; c2 < count[l]; ++c2) ml[cc >> (l - root)] = (uint8_t)l, ++cc;
+			cc <<= 1;
+		}
+	}
+	unsigned next_sub = 1u << root, cur = ~0u, sub = 0, sbits = 0;
+	for (unsigned l = root + 1; l <= maxlen; ++l) {
+		for (unsigned c2 = 0; c2 < count[l]; ++c2) {
+			const unsigned s = sorted[idx++];
+			const unsigned pre = code >> (l - root);
+			if (pre != cur) {
+				cur = pre;
+				sbits = ml[pre] - root;
+				sub = next_sub;
+				next_sub += 1u << sbits;
+				for (unsigned i = 0; i < (1u << sbits); ++i) T[sub + i] = bad;
+				T[rev(pre, root)] = mk(root, sbits, K_SUB, sub);
+			}
+			const unsigned lo = l - root;
+			const uint32_t e = sym_entry(c, s, l);
+			for (unsigned k = rev(code & ((1u << lo) - 1), lo); k < (1u << sbits); k += 1u << lo) T[sub + k] = e;
+			++code;
+		}
+		code <<= 1;
+	}
+	return true;
+}
+
+struct Tables {
+	uint32_t lit[LTAB];
+	uint32_t dist[DTAB];
+};
+
+const Tables &fixed_tables()
+{
+	static Tables *t = [] {
+		Tables *f = new Tables;
+		uint8_t l[288];
+		for (int i = 0; i < 288; ++i) l[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
+		build(f->lit, LROOT, l, 288, C_LIT);
+		uint8_t d[32];
+		memset(d, 5, sizeof d);
+		build(f->dist, DROOT, d, 32, C_DIST);
+		return f;
+	}();
+	return *t;
+}
+
+// Dynamic block header (RFC 1951 3.2.7) into T; false where zlib reports an error.
+bool read_dynamic(BitIn &in, Tables &T)
+{
+	in.refill();
+	const unsigned hlit = in.take(5) + 257, hdist = in.take(5) + 1, hclen = in.take(4) + 4;
+	if (hlit > 286 || hdist > 30) return false;
+	uint8_t cl[19] = {0};
+	for (unsigned i = 0; i < hclen; ++i) {
+		if (in.cnt < 3) in.refill();
+		cl[CL_ORDER[i]] = (uint8_t)in.take(3);
+	}
+	uint32_t ct[1u << CROOT];
+	if (!build(ct, CROOT, cl, 19, C_CL)) return false;
+	uint8_t lens[320];
+	unsigned i = 0;
+	const unsigned total = hlit + hdist;
+	while (i < total) {
+		in.refill();
+		const uint32_t e = ct[in.buf & ((1u << CROOT) - 1)];
+		if (e_kind(e) == K_BAD) return false;
+		in.drop(e_len(e));
+		const unsigned s = e_val(e);
+		if (s < 16) {
+			lens[i++] = (uint8_t)s;
+			continue;
+		}
+		unsigned rep;
+		uint8_t v = 0;
+		if (s == 16) {
+			if (i == 0) return false;
+			v = lens[i - 1];
+			rep = 3 + in.take(2);
+		} else if (s == 17) {
+			rep = 3 + in.take(3);
+		} else {
+			rep = 11 + in.take(7);
+		}
+		if (i + rep > total) return false;
+		memset(lens + i, v, rep);
+		i += rep;
+	}
+	if (in.overrun() || lens[256] == 0) return false;
+	return build(T.lit, LROOT, lens, hlit, C_LIT) && build(T.dist, DROOT, lens + hlit, hdist, C_DIST);
+}
+
+// ---------------------------------------------------------------------------
+// speculative output: 16-bit symbols; MARK | i names byte i of the 32 KiB
+// window that precedes the chunk (i = 32768 - distance before the start)
+// ---------------------------------------------------------------------------
+struct Out {
+	uint16_t *p = nullptr;
+	size_t n = 0, cap = 0;
+	int64_t floor = -(int64_t)WSIZE;   // lowest index a back-reference may reach
+	uint32_t min_mark = WSIZE;         // lowest window index referenced
+	~Out() { free(p); }
+	bool grow(size_t need)
+	{
+		if (need > OUT_CAP + 1024) return false;
+		size_t nc = cap ? cap : ((size_t)1 << 20);
+		while (nc < need) nc *= 2;
+		uint16_t *q = (uint16_t *)realloc(p, nc * sizeof(uint16_t));
+		if (!q) return false;
+		p = q;
+		cap = nc;
+		return true;
+	}
+};
+
+// One Huffman-coded block body up to its end-of-block code.
+bool decode_huff(BitIn &in, const Tables &T, Out &o)
+{
+	for (;;) {
+		if (__builtin_expect(o.cap - o.n < 600, 0) && !o.grow(o.n + 600)) return false;
+		if (__builtin_expect(in.pos > in.n + 16, 0)) return false;
+		in.refill();
+		uint32_t e = T.lit[in.buf & ((1u << LROOT) - 1)];
+		if (e_kind(e) == K_SUB) e = T.lit[e_val(e) + ((in.buf >> LROOT) & ((1u << e_ext(e)) - 1))];
+		in.drop(e_len(e));
+		if (e_kind(e) == K_LIT) {
+			o.p[o.n++] = (uint16_t)e_val(e);
+			// up to two more literals without a refill (56 - 15 >= 2 x 15 + 11)
+			uint32_t e2 = T.lit[in.buf & ((1u << LROOT) - 1)];
+			if (e_kind(e2) != K_LIT) continue;
+			in.drop(e_len(e2));
+			o.p[o.n++] = (uint16_t)e_val(e2);
+			e2 = T.lit[in.buf & ((1u << LROOT) - 1)];
+			if (e_kind(e2) != K_LIT) continue;
+			in.drop(e_len(e2));
+			o.p[o.n++] = (uint16_t)e_val(e2);
+			continue;
+		}
+		if (e_kind(e) == K_EOB) return !in.overrun();
+		if (e_kind(e) != K_LEN) return false;
+		const unsigned len = e_val(e) + in.take(e_ext(e));
+		uint32_t d = T.dist[in.buf & ((1u << DROOT) - 1)];
+		if (e_kind(d) == K_SUB) d = T.dist[e_val(d) + ((in.buf >> DROOT) & ((1u << e_ext(d)) - 1))];
+		if (e_kind(d) == K_BAD) return false;
+		in.drop(e_len(d));
+		const unsigned dist = e_val(d) + in.take(e_ext(d));
+		const int64_t src = (int64_t)o.n - (int64_t)dist;
+		uint16_t *dst = o.p + o.n;
+		if (src >= 0) {
+			const uint16_t *s = dst - dist;
+			if (dist >= 8) {
+				for (unsigned i = 0; i < len; i += 8) memcpy(dst + i, s + i, 16);
+			} else if (dist == 1) {
+				const uint16_t v = s[0];
+				for (unsigned i = 0; i < len; ++i) dst[i] = v;
+			} else {
+				for (unsigned i = 0; i < len; ++i) dst[i] = s[i];
+			}
+		} else {
+			if (src < o.floor) return false;   // before the member's first byte
+			const uint32_t m = (uint32_t)(src + WSIZE);
+			if (m < o.min_mark) o.min_mark = m;
+			for (unsigned i = 0; i < len; ++i) {
+				const int64_t si = src + (int64_t)i;
+				dst[i] = si < 0 ? (uint16_t)(MARK | (uint32_t)(si + WSIZE)) : o.p[si];
+			}
+		}
+		o.n += len;
+	}
+}
+
+// Stored block body; the 3 header bits are consumed.
+bool decode_stored(BitIn &in, Out &o)
+{
+	const uint64_t byte = (in.bitpos() + 7) >> 3;
+	if (byte + 4 > in.n) return false;
+	const unsigned len = in.p[byte] | in.p[byte + 1] << 8, nlen = in.p[byte + 2] | in.p[byte + 3] << 8;
+	if (len != (~nlen & 0xffffu) || byte + 4 + len > in.n) return false;
+	if (o.cap - o.n < (size_t)len + 600 && !o.grow(o.n + len + 600)) return false;
+	const uint8_t *s = in.p + byte + 4;
+	for (unsigned i = 0; i < len; ++i) o.p[o.n + i] = s[i];
+	o.n += len;
+	in.init(in.p, in.n, (byte + 4 + len) * 8);
+	return true;
+}
+
+// RFC 1952 member header at byte `off`: offset of its deflate data, or -1
+// where zlib's inflate would report an error (or the header is cut short).
+int64_t member_header(const uint8_t *p, uint64_t n, uint64_t off)
+{
+	uint64_t q = off;
+	if (q + 10 > n || p[q] != 0x1f || p[q + 1] != 0x8b || p[q + 2] != 8) return -1;
+	const unsigned flg = p[q + 3];
+	if (flg & 0xe0) return -1;
+	q += 10;
+	if (flg & 4) {
+		if (q + 2 > n) return -1;
+		q += 2 + (p[q] | p[q + 1] << 8);
+		if (q > n) return -1;
+	}
+	for (unsigned f = 8; f <= 16; f <<= 1) {
+		if (!(flg & f)) continue;
+		const uint8_t *z = q < n ? (const uint8_t *)memchr(p + q, 0, (size_t)(n - q)) : nullptr;
+		if (!z) return -1;
+		q = (uint64_t)(z - p) + 1;
+	}
+	if (flg & 2) {
+		if (q + 2 > n) return -1;
+		const uint32_t hc = (uint32_t)crc32(0, p + off, (uInt)(q - off)) & 0xffff;
+		if (hc != (uint32_t)(p[q] | p[q + 1] << 8)) return -1;
+		q += 2;
+	}
+	return (int64_t)q;
+}
+
+struct Event {
+	uint64_t off;   // output offset at which a member ended
+	uint32_t crc, isize;
+};
+
+// Speculative chunk decode: blocks from bit `start` until the first block
+// start at or past `end_bit`, across member ends.
+struct Chunk {
+	uint64_t index = ~0ull;
+	uint64_t nom_a = 0, nom_b = 0;    // nominal bit range
+	int64_t start = -1;               // bit where decoding began; -1 none
+	uint64_t end = 0;                 // where it stopped (a block start, or the stream end)
+	bool ok = false, stream_end = false;
+	std::vector<Event> events;
+	Out out;
+	bool busy = false;                // slot in use (decoding, or held until resolved)
+	bool decoded = false;
+	std::unique_ptr<Tables> tab{new Tables};
+};
+
+bool decode_blocks(const uint8_t *p, uint64_t n, BitIn &in, Chunk &C, bool first_checked)
+{
+	Out &o = C.out;
+	bool first = first_checked;
+	for (;;) {
+		const uint64_t at = in.bitpos();
+		if (at >= C.nom_b && !first) {
+			C.end = at;
+			return true;
+		}
+		first = false;
+		in.refill();
+		const unsigned bfinal = in.take(1), btype = in.take(2);
+		bool good;
+		if (btype == 0) good = decode_stored(in, o);
+		else if (btype == 1) good = decode_huff(in, fixed_tables(), o);
+		else if (btype == 2) good = read_dynamic(in, *C.tab) && decode_huff(in, *C.tab, o);
+		else good = false;
+		if (!good) return false;
+		if (!bfinal) continue;
+		uint64_t byte = (in.bitpos() + 7) >> 3;
+		if (byte + 8 > n) return false;
+		C.events.push_back({o.n, le32(p + byte), le32(p + byte + 4)});
+		byte += 8;
+		if (n - byte < 2 || p[byte] != 0x1f || p[byte + 1] != 0x8b) {   // end, or trailing garbage
+			C.stream_end = true;
+			C.end = byte * 8;
+			return true;
+		}
+		const int64_t d = member_header(p, n, byte);
+		if (d < 0) return false;
+		o.floor = (int64_t)o.n;
+		in.init(p, n, (uint64_t)d * 8);
+	}
+}
+
+// Cheap tests on a candidate dynamic block header at bit b: block type,
+// symbol counts and a complete code-length code.
+inline bool quick_dynamic(const uint8_t *p, uint64_t n, uint64_t b)
+{
+	const uint64_t byte = b >> 3;
+	if (byte + 8 > n) return false;
+	uint64_t w;
+	memcpy(&w, p + byte, 8);
+	w >>= (b & 7);
+	if ((w & 6) != 4) return false;
+	if (((w >> 3) & 31) > 29 || ((w >> 8) & 31) > 29) return false;
+	const unsigned hclen = (unsigned)((w >> 13) & 15) + 4;
+	const uint64_t b2 = b + 17, byte2 = b2 >> 3;
+	if (byte2 + 8 > n) return false;
+	uint64_t w2;
+	memcpy(&w2, p + byte2, 8);
+	w2 >>= (b2 & 7);
+	unsigned kraft = 0;
+	for (unsigned i = 0; i < hclen; ++i) {
+		const unsigned l = (unsigned)(w2 >> (3 * i)) & 7;
+		if (l) kraft += 128u >> l;
+	}
+	return kraft == 128;
+}
+
+// Plausible block header at bit b (the block after a candidate): stored with
+// matching LEN/NLEN, fixed, or a dynamic header that builds.
+bool plausible_next(const uint8_t *p, uint64_t n, uint64_t b, Tables &scratch)
+{
+	BitIn in;
+	in.init(p, n, b);
+	in.take(1);
+	const unsigned bt = in.take(2);
+	if (bt == 1) return true;
+	if (bt == 3) return false;
+	if (bt == 0) {
+		const uint64_t byte = (in.bitpos() + 7) >> 3;
+		if (byte + 4 > n) return false;
+		return (p[byte] | p[byte + 1] << 8) == (~(p[byte + 2] | p[byte + 3] << 8) & 0xffff);
+	}
+	return read_dynamic(in, scratch);
+}
+
+void decode_chunk(const uint8_t *p, uint64_t n, uint64_t first_bit, Chunk &C)
+{
+	C.ok = C.stream_end = false;
+	C.start = -1;
+	C.events.clear();
+	Out &o = C.out;
+	o.n = 0;
+	o.min_mark = WSIZE;
+	BitIn in;
+	if (C.index == 0) {   // the stream's start: known (empty) history
+		o.floor = 0;
+		C.start = (int64_t)first_bit;
+		in.init(p, n, first_bit);
+		C.ok = decode_blocks(p, n, in, C, true);
+		return;
+	}
+	const uint64_t lim = std::min(C.nom_b, n * 8);
+	Tables scratch;
+	const double t0 = gz_now();
+	for (uint64_t b = C.nom_a; b < lim; ++b) {
+		if (!quick_dynamic(p, n, b)) continue;
+		o.n = 0;
+		o.floor = -(int64_t)WSIZE;
+		o.min_mark = WSIZE;
+		C.events.clear();
+		in.init(p, n, b);
+		in.take(3);
+		if (!read_dynamic(in, *C.tab) || !decode_huff(in, *C.tab, o)) continue;
+		// the candidate block decoded; its header bit said whether it was final
+		BitIn h;
+		h.init(p, n, b);
+		const bool final_blk = h.take(1);
+		if (!final_blk && !plausible_next(p, n, in.bitpos(), scratch)) continue;
+		C.start = (int64_t)b;
+		const double t1 = gz_now();
+		prof_search_us += (uint64_t)((t1 - t0) * 1e6);
+		struct Acc {
+			double t;
+			~Acc() { prof_decode_us += (uint64_t)((gz_now() - t) * 1e6); }
+		} acc{t1};
+		if (final_blk) {   // continue through the trailer like decode_blocks
+			uint64_t byte = (in.bitpos() + 7) >> 3;
+			if (byte + 8 > n) return;
+			C.events.push_back({o.n, le32(p + byte), le32(p + byte + 4)});
+			byte += 8;
+			if (n - byte < 2 || p[byte] != 0x1f || p[byte + 1] != 0x8b) {
+				C.stream_end = true;
+				C.end = byte * 8;
+				C.ok = true;
+				return;
+			}
+			const int64_t d = member_header(p, n, byte);
+			if (d < 0) return;
+			o.floor = (int64_t)o.n;
+			in.init(p, n, (uint64_t)d * 8);
+		}
+		C.ok = decode_blocks(p, n, in, C, false);
+		return;
+	}
+}
+
+// ---------------------------------------------------------------------------
+// resolved output handed to the reader
+// ---------------------------------------------------------------------------
+struct Piece {
+	uint8_t *text = nullptr;
+	size_t n = 0, cap = 0;
+	Chunk *src = nullptr;             // symbols still to resolve (accepted chunk)
+	std::vector<uint8_t> window;      // the 32 KiB before src's first symbol
+	std::vector<Event> events;
+	std::vector<uint32_t> seg_crc;    // events.size() + 1 segments
+	bool stream_end = false;
+	bool ready = false, resolving = false;
+	~Piece() { free(text); }
+	bool reserve(size_t c)
+	{
+		if (c <= cap) return true;
+		uint8_t *q = (uint8_t *)realloc(text, c);
+		if (!q) return false;
+		text = q;
+		cap = c;
+		return true;
+	}
+};
+
+void resolve(Piece &P)
+{
+	const Chunk &C = *P.src;
+	const uint16_t *s = C.out.p;
+	const size_t n = C.out.n;
+	uint8_t *t = P.text;
+	const uint8_t *w = P.window.data();
+	size_t i = 0;
+	for (; i + 32 <= n; i += 32) {
+		uint16_t acc = 0;
+		for (int k = 0; k < 32; ++k) acc |= s[i + k];
+		if (acc < 256) {
+			for (int k = 0; k < 32; ++k) t[i + k] = (uint8_t)s[i + k];
+		} else {
+			for (int k = 0; k < 32; ++k) {
+				const uint16_t v = s[i + k];
+				t[i + k] = v < 256 ? (uint8_t)v : w[v & (WSIZE - 1)];
+			}
+		}
+	}
+	for (; i < n; ++i) t[i] = s[i] < 256 ? (uint8_t)s[i] : w[s[i] & (WSIZE - 1)];
+	P.n = n;
+}
+
+void piece_crcs(Piece &P)
+{
+	P.seg_crc.clear();
+	uint64_t a = 0;
+	for (const Event &e : P.events) {
+		P.seg_crc.push_back((uint32_t)crc32(0, P.text + a, (uInt)(e.off - a)));
+		a = e.off;
+	}
+	uint32_t c = 0;
+	for (uint64_t x = a; x < P.n;) {   // crc32's length is 32-bit
+		const uint64_t m = std::min<uint64_t>(P.n - x, (uint64_t)1 << 30);
+		c = (uint32_t)crc32(c, P.text + x, (uInt)m);
+		x += m;
+	}
+	P.seg_crc.push_back(c);
+}
+
+} // namespace
+
+class VcGzParallel {
+public:
+	~VcGzParallel() { shutdown(); }
+	bool start(const char *path, int threads, uint64_t chunk_bytes);
+	int64_t read(uint8_t *dst, size_t n);
+	void get_stats(VcGzStats *st)
+	{
+		std::lock_guard<std::mutex> lk(mu_);
+		*st = stats;
+	}
+
+private:
+	VcGzStats stats;                  // guarded by mu_ (out_bytes, members, crc_error: reader thread)
+	// input
+	int fd_ = -1;
+	const uint8_t *p_ = nullptr;
+	uint64_t n_ = 0, first_bit_ = 0, chunk_bits_ = 0, nchunks_ = 0;
+	// shared state
+	std::mutex mu_;
+	std::condition_variable cv_;
+	bool stop_ = false, seq_done_ = false;
+	std::vector<std::unique_ptr<Chunk>> slots_;
+	uint64_t next_decode_ = 0;
+	std::deque<std::unique_ptr<Piece>> pieces_;
+	std::vector<std::unique_ptr<Piece>> spare_;
+	size_t max_pieces_ = 8;
+	std::vector<std::thread> workers_;
+	std::thread seq_;
+	// sequencer state
+	std::vector<uint8_t> window_ = std::vector<uint8_t>(WSIZE);
+	uint64_t member_text_ = 0;        // bytes of the current member so far
+	// reader state
+	Piece *cur_ = nullptr;
+	size_t rd_ = 0, ev_ = 0, seg_a_ = 0;
+	uint32_t mcrc_ = 0;
+	uint64_t mlen_ = 0;
+	bool done_ = false;
+
+	void worker();
+	void sequencer();
+	bool fallback(uint64_t &expect, uint64_t nom_b, bool &ended);
+	Piece *new_piece();
+	bool push_piece(std::unique_ptr<Piece> P);   // waits for queue space; false on stop
+	void window_append(const uint8_t *t, size_t n);
+	void shutdown();
+};
+
+Piece *VcGzParallel::new_piece()
+{
+	std::lock_guard<std::mutex> lk(mu_);
+	if (!spare_.empty()) {
+		Piece *P = spare_.back().release();
+		spare_.pop_back();
+		P->n = 0;
+		P->src = nullptr;
+		P->events.clear();
+		P->seg_crc.clear();
+		P->stream_end = P->ready = P->resolving = false;
+		return P;
+	}
+	return new Piece;
+}
+
+bool VcGzParallel::push_piece(std::unique_ptr<Piece> P)
+{
+	std::unique_lock<std::mutex> lk(mu_);
+	cv_.wait(lk, [&] { return stop_ || pieces_.size() < max_pieces_; });
+	if (stop_) return false;
+	pieces_.push_back(std::move(P));
+	cv_.notify_all();
+	return true;
+}
+
+void VcGzParallel::window_append(const uint8_t *t, size_t n)
+{
+	uint8_t *w = window_.data();
+	if (n >= WSIZE) {
+		memcpy(w, t + n - WSIZE, WSIZE);
+	} else if (n) {
+		memmove(w, w + n, WSIZE - n);
+		memcpy(w + WSIZE - n, t, n);
+	}
+}
+
+void VcGzParallel::worker()
+{
+	for (;;) {
+		std::unique_lock<std::mutex> lk(mu_);
+		Piece *task = nullptr;
+		Chunk *dec = nullptr;
+		cv_.wait(lk, [&] {
+			if (stop_) return true;
+			for (auto &P : pieces_)
+				if (P->src && !P->resolving) {
+					task = P.get();
+					return true;
+				}
+			if (next_decode_ < nchunks_) {
+				Chunk &C = *slots_[next_decode_ % slots_.size()];
+				if (!C.busy) {
+					dec = &C;
+					return true;
+				}
+			}
+			return false;
+		});
+		if (stop_) return;
+		if (task) {
+			task->resolving = true;
+			lk.unlock();
+			bool ok = task->reserve(task->src->out.n + 64);
+			if (ok) {
+				const double r0 = gz_now();
+				resolve(*task);
+				const double r1 = gz_now();
+				piece_crcs(*task);
+				prof_resolve_us += (uint64_t)((r1 - r0) * 1e6);
+				prof_crc_us += (uint64_t)((gz_now() - r1) * 1e6);
+			}
+			lk.lock();
+			task->src->busy = false;
+			task->src = nullptr;
+			if (!ok) {   // out of memory: the stream ends before this piece
+				task->n = 0;
+				task->events.clear();
+				task->seg_crc.assign(1, 0);
+				task->stream_end = true;
+			}
+			task->ready = true;
+			cv_.notify_all();
+			continue;
+		}
+		const uint64_t j = next_decode_++;
+		dec->busy = true;
+		dec->decoded = false;
+		dec->index = j;
+		dec->nom_a = first_bit_ + j * chunk_bits_;
+		dec->nom_b = j + 1 == nchunks_ ? n_ * 8 : first_bit_ + (j + 1) * chunk_bits_;
+		lk.unlock();
+		decode_chunk(p_, n_, first_bit_, *dec);
+		lk.lock();
+		dec->decoded = true;
+		cv_.notify_all();
+	}
+}
+
+// zlib from the true boundary `expect` with the true history, until the first
+// block start at or past nom_b, the end of the stream, or an error.  Output
+// goes to pieces of at most PIECE_CAP bytes.  false only on stop / no memory.
+bool VcGzParallel::fallback(uint64_t &expect, uint64_t nom_b, bool &ended)
+{
+	z_stream zs;
+	memset(&zs, 0, sizeof zs);
+	if (inflateInit2(&zs, -15) != Z_OK) return false;
+	uint64_t byte = expect >> 3;
+	const unsigned sh = (unsigned)(expect & 7);
+	if (sh) {
+		inflatePrime(&zs, (int)(8 - sh), p_[byte] >> sh);
+		++byte;
+	}
+	const size_t dict = (size_t)std::min<uint64_t>(member_text_, WSIZE);
+	if (dict) inflateSetDictionary(&zs, window_.data() + WSIZE - dict, (uInt)dict);
+	const uint8_t *in = p_ + byte;
+	auto feed = [&]() {
+		zs.next_in = (Bytef *)in;
+		zs.avail_in = (uInt)std::min<uint64_t>(n_ - (uint64_t)(in - p_), (uint64_t)1 << 30);
+	};
+	feed();
+	std::unique_ptr<Piece> P(new_piece());
+	auto emit = [&](bool last) -> bool {
+		P->stream_end = last;
+		piece_crcs(*P);
+		P->ready = true;
+		return push_piece(std::move(P));
+	};
+	bool alive = P->reserve(PIECE_CAP);
+	while (alive) {
+		if (P->n == P->cap) {   // piece full
+			if (!emit(false)) {
+				alive = false;
+				break;
+			}
+			P.reset(new_piece());
+			if (!P->reserve(PIECE_CAP)) {
+				alive = false;
+				break;
+			}
+		}
+		zs.next_out = P->text + P->n;
+		zs.avail_out = (uInt)(P->cap - P->n);
+		const int ret = inflate(&zs, Z_BLOCK);
+		const size_t made = (size_t)(zs.next_out - (P->text + P->n));
+		window_append(P->text + P->n, made);
+		P->n += made;
+		member_text_ += made;
+		in = zs.next_in;
+		if (ret == Z_STREAM_END) {   // member end: trailer, then another member or the end
+			uint64_t tb = (uint64_t)(in - p_);
+			if (tb + 8 > n_) {   // trailer cut short: gzread's "unexpected end of file"
+				ended = true;
+				break;
+			}
+			P->events.push_back({P->n, le32(p_ + tb), le32(p_ + tb + 4)});
+			tb += 8;
+			const int64_t d = (n_ - tb >= 2 && p_[tb] == 0x1f && p_[tb + 1] == 0x8b) ? member_header(p_, n_, tb) : -1;
+			if (d < 0) {   // no further member (trailing bytes ignored), or a header zlib rejects
+				ended = true;
+				break;
+			}
+			member_text_ = 0;
+			inflateReset(&zs);
+			in = p_ + d;
+			feed();
+			if ((uint64_t)d * 8 >= nom_b) {
+				expect = (uint64_t)d * 8;
+				break;
+			}
+			continue;
+		}
+		if (ret != Z_OK && ret != Z_BUF_ERROR) {   // corrupt data: the output so far, then the end
+			ended = true;
+			break;
+		}
+		if (zs.avail_in == 0) {
+			if ((uint64_t)(in - p_) >= n_) {
+				if (ret == Z_BUF_ERROR) {   // input exhausted inside the stream
+					ended = true;
+					break;
+				}
+			} else {
+				feed();
+			}
+		} else if (ret == Z_BUF_ERROR && zs.avail_out != 0) {
+			ended = true;   // no progress with input and room: treat as corrupt
+			break;
+		}
+		if ((zs.data_type & 192) == 128) {   // at the start of a block (not after the final one)
+			const uint64_t at = (uint64_t)(in - p_) * 8 - (uint64_t)(zs.data_type & 7);
+			if (at >= nom_b) {
+				expect = at;
+				break;
+			}
+		}
+	}
+	inflateEnd(&zs);
+	if (!alive) return false;
+	if (P->n == 0 && P->events.empty() && !ended) {
+		std::lock_guard<std::mutex> lk(mu_);
+		spare_.push_back(std::move(P));
+		return true;
+	}
+	return emit(ended);
+}
+
+void VcGzParallel::sequencer()
+{
+	uint64_t expect = first_bit_;
+	bool ended = false;
+	for (uint64_t j = 0; j < nchunks_ && !ended; ++j) {
+		Chunk *C = slots_[j % slots_.size()].get();
+		{
+			std::unique_lock<std::mutex> lk(mu_);
+			cv_.wait(lk, [&] { return stop_ || (C->index == j && C->decoded); });
+			if (stop_) break;
+		}
+		if (expect >= C->nom_b) {
+			std::lock_guard<std::mutex> lk(mu_);
+			C->busy = false;
+			++stats.skipped;  // under mu_
+			cv_.notify_all();
+			continue;
+		}
+		const uint64_t have = std::min<uint64_t>(member_text_, WSIZE);
+		const bool take = C->ok && C->start >= 0 && (uint64_t)C->start == expect &&
+		                  C->out.min_mark >= WSIZE - have;
+		if (take) {
+			std::unique_ptr<Piece> P(new_piece());
+			P->src = C;
+			P->window = window_;
+			P->events = C->events;
+			P->stream_end = C->stream_end;
+			// the window after this chunk: its last 32 KiB, markers resolved
+			const uint16_t *s = C->out.p;
+			const size_t n = C->out.n;
+			uint8_t tail[WSIZE];
+			const size_t tn = std::min<size_t>(n, WSIZE);
+			for (size_t i = 0; i < tn; ++i) {
+				const uint16_t v = s[n - tn + i];
+				tail[i] = v < 256 ? (uint8_t)v : window_[v & (WSIZE - 1)];
+			}
+			window_append(tail, tn);
+			member_text_ = C->events.empty() ? member_text_ + n : n - C->events.back().off;
+			expect = C->end;
+			ended = C->stream_end;
+			{
+				std::lock_guard<std::mutex> lk(mu_);
+				++stats.accepted;
+			}
+			if (!push_piece(std::move(P))) break;
+			continue;
+		}
+		{
+			std::lock_guard<std::mutex> lk(mu_);
+			C->busy = false;
+			++stats.fallback;
+			cv_.notify_all();
+		}
+		if (!fallback(expect, C->nom_b, ended)) break;
+	}
+	std::lock_guard<std::mutex> lk(mu_);
+	seq_done_ = true;
+	cv_.notify_all();
+}
+
+bool VcGzParallel::start(const char *path, int threads, uint64_t chunk_bytes)
+{
+	fd_ = open(path, O_RDONLY);
+	if (fd_ < 0) return false;
+	struct stat sb;
+	if (fstat(fd_, &sb) != 0 || !S_ISREG(sb.st_mode) || sb.st_size < 18) return false;
+	n_ = (uint64_t)sb.st_size;
+	void *m = mmap(nullptr, (size_t)n_, PROT_READ, MAP_PRIVATE, fd_, 0);
+	if (m == MAP_FAILED) return false;
+	p_ = (const uint8_t *)m;
+	madvise(m, (size_t)n_, MADV_SEQUENTIAL);
+	const int64_t d = member_header(p_, n_, 0);
+	if (d < 0) return false;
+	first_bit_ = (uint64_t)d * 8;
+	if (chunk_bytes < 1024) chunk_bytes = 1024;
+	chunk_bits_ = chunk_bytes * 8;
+	nchunks_ = (n_ * 8 - first_bit_ + chunk_bits_ - 1) / chunk_bits_;
+	if (nchunks_ == 0) nchunks_ = 1;
+	stats.chunks = nchunks_;
+	if (threads < 1) threads = 1;
+	slots_.resize((size_t)threads + 2);
+	for (auto &s : slots_) s.reset(new Chunk);
+	max_pieces_ = (size_t)threads + 4;
+	fixed_tables();
+	for (int t = 0; t < threads; ++t) workers_.emplace_back(&VcGzParallel::worker, this);
+	seq_ = std::thread(&VcGzParallel::sequencer, this);
+	return true;
+}
+
+int64_t VcGzParallel::read(uint8_t *dst, size_t n)
+{
+	size_t got = 0;
+	while (got < n && !done_) {
+		if (!cur_) {
+			std::unique_lock<std::mutex> lk(mu_);
+			cv_.wait(lk, [&] { return (!pieces_.empty() && pieces_.front()->ready) || (seq_done_ && pieces_.empty()); });
+			if (pieces_.empty()) {
+				done_ = true;
+				break;
+			}
+			cur_ = pieces_.front().get();
+			rd_ = ev_ = seg_a_ = 0;
+		}
+		Piece &P = *cur_;
+		const size_t lim = ev_ < P.events.size() ? (size_t)P.events[ev_].off : P.n;
+		const size_t take = std::min(n - got, lim - rd_);
+		memcpy(dst + got, P.text + rd_, take);
+		rd_ += take;
+		got += take;
+		stats.out_bytes += take;
+		if (rd_ != lim) continue;
+		const size_t seg = lim - seg_a_;
+		mcrc_ = (uint32_t)crc32_combine(mcrc_, P.seg_crc[ev_], (z_off_t)seg);
+		mlen_ += seg;
+		seg_a_ = lim;
+		if (ev_ < P.events.size()) {
+			const Event &e = P.events[ev_];
+			if (mcrc_ != e.crc || (uint32_t)mlen_ != e.isize) {   // gzread stops at a failed check
+				stats.crc_error = 1;
+				done_ = true;
+				break;
+			}
+			++stats.members;
+			mcrc_ = 0;
+			mlen_ = 0;
+			++ev_;
+			continue;
+		}
+		const bool last = P.stream_end;
+		{
+			std::lock_guard<std::mutex> lk(mu_);
+			spare_.push_back(std::move(pieces_.front()));
+			pieces_.pop_front();
+			cv_.notify_all();
+		}
+		cur_ = nullptr;
+		if (last) done_ = true;
+	}
+	return (int64_t)got;
+}
+
+void VcGzParallel::shutdown()
+{
+	if (getenv("VAFC_GZ_PROFILE"))
+		fprintf(stderr, "[gzp] thread-seconds: search %.3f decode %.3f resolve %.3f crc %.3f\n", prof_search_us * 1e-6,
+		        prof_decode_us * 1e-6, prof_resolve_us * 1e-6, prof_crc_us * 1e-6);
+	{
+		std::lock_guard<std::mutex> lk(mu_);
+		stop_ = true;
+		cv_.notify_all();
+	}
+	if (seq_.joinable()) seq_.join();
+	for (auto &t : workers_) t.join();
+	workers_.clear();
+	if (p_) munmap((void *)p_, (size_t)n_);
+	p_ = nullptr;
+	if (fd_ >= 0) close(fd_);
+	fd_ = -1;
+}
+
+VcGzParallel *vc_gzp_open(const char *path, int threads, uint64_t chunk_bytes)
+{
+	VcGzParallel *g = new VcGzParallel;
+	if (!g->start(path, threads, chunk_bytes)) {
+		delete g;
+		return nullptr;
+	}
+	return g;
+}
+
+int64_t vc_gzp_read(VcGzParallel *g, uint8_t *dst, size_t n) { return g->read(dst, n); }
+
+void vc_gzp_stats(VcGzParallel *g, VcGzStats *st) { g->get_stats(st); }
+
+void vc_gzp_close(VcGzParallel *g) { delete g; }
+
+// ---------------------------------------------------------------------------
+// host-only test hooks (C ABI): the whole decompressed stream, parallel and
+// through gzread, into caller buffers
+// ---------------------------------------------------------------------------
+extern "C" int64_t vc_gz_inflate_parallel(const char *path, int threads, uint64_t chunk_bytes, uint8_t *out,
+                                          uint64_t cap, uint64_t *stats6)
+{
+	VcGzParallel *g = vc_gzp_open(path, threads, chunk_bytes);
+	if (!g) return -1;
+	uint64_t tot = 0;
+	std::vector<uint8_t> tmp((size_t)1 << 20);
+	for (;;) {
+		const int64_t r = g->read(tmp.data(), tmp.size());
+		if (r <= 0) break;
+		if (out && tot < cap) memcpy(out + tot, tmp.data(), (size_t)std::min<uint64_t>((uint64_t)r, cap - tot));
+		tot += (uint64_t)r;
+	}
+	if (stats6) {
+		VcGzStats s;
+		g->get_stats(&s);
+		stats6[0] = s.chunks;
+		stats6[1] = s.accepted;
+		stats6[2] = s.skipped;
+		stats6[3] = s.fallback;
+		stats6[4] = s.members;
+		stats6[5] = (uint64_t)s.crc_error;
+	}
+	vc_gzp_close(g);
+	return (int64_t)tot;
+}
+
+extern "C" int64_t vc_gz_inflate_zlib(const char *path, uint8_t *out, uint64_t cap)
+{
+	gzFile f = gzopen(path, "r");
+	if (!f) return -1;
+	uint64_t tot = 0;
+	std::vector<uint8_t> tmp((size_t)1 << 20);
+	for (;;) {
+		const int r = gzread(f, tmp.data(), (unsigned)tmp.size());
+		if (r <= 0) break;
+		if (out && tot < cap) memcpy(out + tot, tmp.data(), (size_t)std::min<uint64_t>((uint64_t)r, cap - tot));
+		tot += (uint64_t)r;
+	}
+	gzclose(f);
+	return (int64_t)tot;
+}

@@ -683,32 +683,6 @@ double wall_now()
 
 } // namespace
 
-// The reference's per-file block loop.  kt_pipeline(3 workers) runs
-// worker_pipeline's step 0 strictly in block order and each worker retires on
-// the first empty block it reads, so a file ends at its third empty block
-// (kthread.c:97-128, vaf-counter.c:486-517).  Reads shorter than k are
-// skipped and not counted; a -1/-2 from the reader ends the current block.
-template <class Sink>
-static int block_loop(VcFastqReader &rd, int k, int block_bases, Sink &&sink, vc_file_stats &st)
-{
-	int empty = 0, rc = VC_OK;
-	while (empty < 3 && rc == VC_OK) {
-		int64_t sum = 0;
-		int ret;
-		while ((ret = rd.next()) >= 0) {
-			if (ret < k) continue;
-			if ((rc = sink(rd.seq(), (size_t)ret)) != VC_OK) break;
-			sum += ret;
-			st.bases += (uint64_t)ret;
-			st.seqs += 1;
-			if (sum >= block_bases) break;
-		}
-		if (sum == 0) ++empty;
-		else ++st.blocks;
-	}
-	return rc;
-}
-
 // ---------------------------------------------------------------------------
 // parallel ingest of plain files (vafc_ingest.h): pieces parsed by -t worker
 // threads straight into pinned slots, shipped to the device in file order
@@ -860,10 +834,10 @@ extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n
 		}
 		close(fd);
 	}
-	VcFastqReader rd;
-	if (!rd.open(path)) return VC_EIO;
+	VcFastqReader rd;   // gzip: inflated by n_threads workers (vafc_gzip.h)
+	if (!rd.open_parallel(path, clamp_threads(n_threads))) return VC_EIO;
 	BatchWriter bw(c);
-	int rc = block_loop(rd, c->k, block_bases,
+	int rc = vc_block_loop(rd, c->k, block_bases,
 	                    [&bw](const char *s, size_t l) { return bw.add(s, l); }, local);
 	if (rc == VC_OK) rc = bw.flush();
 	if (rc == VC_OK) HIPCK(hipStreamSynchronize(c->st));
@@ -881,7 +855,7 @@ extern "C" int vc_scan_file(const char *path, int k, int block_bases, vc_file_st
 	VcFastqReader rd;
 	if (!rd.open(path)) return VC_EIO;
 	size_t nb = 0, nr = 0;
-	int rc = block_loop(rd, k, block_bases, [&](const char *s, size_t l) {
+	int rc = vc_block_loop(rd, k, block_bases, [&](const char *s, size_t l) {
 		if (seq_out && nb + l <= seq_cap) memcpy(seq_out + nb, s, l);
 		if (lens_out && nr < lens_cap) lens_out[nr] = (uint32_t)l;
 		nb += l;

@@ -408,8 +408,22 @@ extern "C" int vc_scan_file_parallel(const char *path, int k, int block_bases, i
 	}
 	uint8_t magic[2] = {0, 0};
 	if (pread_full(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b) {
+		// gzip: n_threads inflate workers (piece_bytes compressed bytes per
+		// chunk), the block loop over the inflated stream in this thread
 		close(fd);
-		return VC_EINVAL;   // gzip: sequential reader only
+		VcFastqReader rd;
+		if (!rd.open_parallel(path, n_threads, piece_bytes)) return VC_EIO;
+		size_t nb = 0, nr = 0;
+		const int rc = vc_block_loop(rd, k, block_bases, [&](const char *q, size_t l) {
+			if (seq_out && nb + l <= seq_cap) memcpy(seq_out + nb, q, l);
+			if (lens_out && nr < lens_cap) lens_out[nr] = (uint32_t)l;
+			nb += l;
+			++nr;
+			return VC_OK;
+		}, local);
+		local.seconds = mono_now() - t0;
+		*st = local;
+		return rc;
 	}
 	HostSink sink(n_threads + 2, piece_bytes, seq_out, seq_cap, lens_out, lens_cap);
 	const int rc = vc_ingest_plain(fd, (uint64_t)sb.st_size, k, block_bases, n_threads, n_threads + 2,

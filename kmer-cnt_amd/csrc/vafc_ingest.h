@@ -31,6 +31,34 @@
 #include <stdint.h>
 
 #include "vafc.h"
+#include "vafc_fastq.h"
+
+// The reference's per-file block loop.  kt_pipeline(3 workers) runs
+// worker_pipeline's step 0 strictly in block order and each worker retires on
+// the first empty block it reads, so a file ends at its third empty block
+// (kthread.c:97-128, vaf-counter.c:486-517).  Reads shorter than k are
+// skipped and not counted; a -1/-2 from the reader ends the current block.
+template <class Sink>
+inline int vc_block_loop(VcFastqReader &rd, int k, int block_bases, Sink &&sink, vc_file_stats &st)
+{
+	int empty = 0, rc = VC_OK;
+	while (empty < 3 && rc == VC_OK) {
+		int64_t sum = 0;
+		int ret;
+		while ((ret = rd.next()) >= 0) {
+			if (ret < k) continue;
+			if ((rc = sink(rd.seq(), (size_t)ret)) != VC_OK) break;
+			sum += ret;
+			st.bases += (uint64_t)ret;
+			st.seqs += 1;
+			if (sum >= block_bases) break;
+		}
+		if (sum == 0) ++empty;
+		else ++st.blocks;
+	}
+	return rc;
+}
+
 
 struct VcSlotBuf {
 	uint8_t *seq = nullptr;       // accepted reads, concatenated

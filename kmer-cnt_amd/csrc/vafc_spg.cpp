@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "vafc.h"
@@ -38,8 +39,11 @@ extern "C" int vc_fasta_load(const char *path, vc_fasta **out)
 {
 	if (!path || !out) return VC_EINVAL;
 	*out = nullptr;
-	VcFastqReader rd;
-	if (!rd.open(path)) return VC_EIO;
+	VcFastqReader rd;   // a gzip genome is inflated in parallel (vafc_gzip.h)
+	const char *te = getenv("VAFC_THREADS");
+	int threads = te && atoi(te) > 0 ? atoi(te) : (int)std::thread::hardware_concurrency();
+	threads = threads < 1 ? 1 : (threads > 16 ? 16 : threads);
+	if (!rd.open_parallel(path, threads)) return VC_EIO;
 	rd.keep_names(true);
 	vc_fasta *fa = new (std::nothrow) vc_fasta;
 	if (!fa) return VC_ENOMEM;

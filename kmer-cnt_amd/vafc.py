@@ -37,6 +37,7 @@ EXPORTS = (
     "vc_count_block", "vc_count_device", "vc_finish", "vc_reset", "vc_device_counts",
     "vc_bind_outputs", "vc_device_tally", "vc_stream", "vc_set_timing", "vc_kernel_ms",
     "vc_table_info", "vc_count_file", "vc_scan_file", "vc_scan_file_parallel", "vc_scan_records", "vc_reserve_file_ingest",
+    "vc_gz_inflate_parallel", "vc_gz_inflate_zlib",
     "vc_fasta_load", "vc_fasta_count", "vc_fasta_name", "vc_fasta_seq", "vc_fasta_data", "vc_fasta_free",
     "vc_count_candidates", "vc_set_nt4_decode",
     "vc_synth_reads",
@@ -109,6 +110,8 @@ def lib():
         "vc_scan_file_parallel": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_uint64,
                                             C.POINTER(FileStats), P, C.c_size_t, P, C.c_size_t]),
         "vc_scan_records": (C.c_int64, [C.c_char_p, P, C.c_int64]),
+        "vc_gz_inflate_parallel": (C.c_int64, [C.c_char_p, C.c_int, C.c_uint64, P, C.c_uint64, P]),
+        "vc_gz_inflate_zlib": (C.c_int64, [C.c_char_p, P, C.c_uint64]),
         "vc_reserve_file_ingest": (C.c_int, [P, C.c_int]),
         "vc_fasta_load": (C.c_int, [C.c_char_p, C.POINTER(P)]),
         "vc_fasta_count": (C.c_int, [P]),
@@ -321,7 +324,7 @@ def scan_file(fn: str, k: int, block_size: int = 10_000_000, with_reads: bool = 
         rc = lib().vc_scan_file(fn.encode(), k, block_size, C.byref(st), None, 0, None, 0)
         reads = None
     else:
-        size = os.path.getsize(fn) + 16
+        size = _text_size(fn) + 16
         seq = np.zeros(max(size * 4, 64), np.uint8)     # gz inflates; bounded by caller use
         lens = np.zeros(max(size, 16), np.uint32)
         rc = lib().vc_scan_file(fn.encode(), k, block_size, C.byref(st), _ptr(seq), seq.size,
@@ -338,17 +341,53 @@ def scan_file(fn: str, k: int, block_size: int = 10_000_000, with_reads: bool = 
     return st, reads
 
 
+def _text_size(fn: str) -> int:
+    """Bytes of the file's (decompressed) text."""
+    with open(fn, "rb") as f:
+        gz = f.read(2) == b"\x1f\x8b"
+    if not gz:
+        return os.path.getsize(fn)
+    n = lib().vc_gz_inflate_zlib(fn.encode(), None, 0)
+    return max(int(n), 0)
+
+
+def gz_inflate_parallel(fn: str, threads: int = 4, chunk_bytes: int = 4 << 20):
+    """The decompressed stream of a gzip file through the parallel inflater
+    (vafc_gzip.h): (bytes, stats dict); None if the inflater declines the file."""
+    st = np.zeros(6, np.uint64)
+    n = lib().vc_gz_inflate_parallel(fn.encode(), threads, chunk_bytes, None, 0, _ptr(st))
+    if n < 0:
+        return None
+    cap = int(n) + 1
+    out = np.zeros(cap, np.uint8)
+    n = lib().vc_gz_inflate_parallel(fn.encode(), threads, chunk_bytes, _ptr(out), cap, _ptr(st))
+    keys = ("chunks", "accepted", "skipped", "fallback", "members", "crc_error")
+    return out[:min(int(n), cap)].tobytes(), dict(zip(keys, (int(x) for x in st)))
+
+
+def gz_inflate_zlib(fn: str) -> bytes:
+    """The decompressed stream through zlib's gzread (the reference's reader)."""
+    cap = _text_size(fn) + 1
+    out = np.zeros(cap, np.uint8)
+    n = lib().vc_gz_inflate_zlib(fn.encode(), _ptr(out), cap)
+    if n < 0:
+        raise FileNotFoundError(fn)
+    return out[:int(n)].tobytes()
+
+
 def scan_file_parallel(fn: str, k: int, block_size: int = 10_000_000, threads: int = 4,
                        piece_bytes: int = 8 << 20, with_reads: bool = False):
-    """Host-only parallel reader of vc_count_file for plain files (no device):
-    (FileStats, reads or None); the reads are those of scan_file, in order."""
+    """Host-only parallel reader of vc_count_file (no device): (FileStats, reads
+    or None); the reads are those of scan_file, in order.  Plain files: pieces
+    of piece_bytes parsed by `threads` workers; gzip: `threads` inflate workers
+    on chunks of piece_bytes compressed bytes, one parsing thread."""
     st = FileStats()
     if not with_reads:
         rc = lib().vc_scan_file_parallel(fn.encode(), k, block_size, threads, piece_bytes, C.byref(st),
                                          None, 0, None, 0)
         reads = None
     else:
-        size = os.path.getsize(fn) + 16
+        size = _text_size(fn) + 16
         seq = np.zeros(max(size, 64), np.uint8)
         lens = np.zeros(max(size, 16), np.uint32)
         rc = lib().vc_scan_file_parallel(fn.encode(), k, block_size, threads, piece_bytes, C.byref(st),

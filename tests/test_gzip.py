@@ -1,0 +1,233 @@
+"""The parallel gzip inflater (vafc_gzip.cpp) against zlib's gzread, the
+reference's reader of .gz input (vaf-counter.c:12,557): identical byte
+streams for every compression level and strategy, multi-member files, header
+options, trailing bytes and truncated files, at chunk sizes from 1 KiB up;
+the speculative path is checked to be the one that runs (accepted chunks),
+and the FASTQ reader on top of it against the sequential gzread reader."""
+import gzip
+import os
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+
+def _fastq_text(rng, n, L=150):
+    out = []
+    for i in range(n):
+        seq = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, L)].tobytes()
+        if i % 37 == 0:
+            seq = seq[:40] + b"N" * 5 + seq[45:]
+        out.append(b"@r%d extra\n%s\n+\n%s\n" % (i, seq, b"I" * L))
+    return b"".join(out)
+
+
+def _member(data, level=6, strategy=zlib.Z_DEFAULT_STRATEGY, flags=0, extra=b"", name=b"", comment=b"",
+            mem_level=8):
+    """One RFC 1952 member with the given header options."""
+    hdr = bytearray(b"\x1f\x8b\x08" + bytes([flags]) + b"\x00\x00\x00\x00\x00\x03")
+    if flags & 4:
+        hdr += struct.pack("<H", len(extra)) + extra
+    if flags & 8:
+        hdr += name + b"\x00"
+    if flags & 16:
+        hdr += comment + b"\x00"
+    if flags & 2:
+        hdr += struct.pack("<H", zlib.crc32(bytes(hdr)) & 0xffff)
+    c = zlib.compressobj(level, zlib.DEFLATED, -15, mem_level, strategy)
+    body = c.compress(data) + c.flush()
+    return bytes(hdr) + body + struct.pack("<II", zlib.crc32(data) & 0xffffffff, len(data) & 0xffffffff)
+
+
+def _check(path, threads=4, chunks=(1024, 4096, 65536, 1 << 22), want_accept=False):
+    import vafc
+    ref = vafc.gz_inflate_zlib(path)
+    for ch in chunks:
+        got = vafc.gz_inflate_parallel(path, threads=threads, chunk_bytes=ch)
+        assert got is not None, (path, ch)
+        data, st = got
+        assert len(data) == len(ref) and data == ref, (path, ch, len(data), len(ref), st)
+        if want_accept and st["chunks"] > 2:   # the speculative path ran
+            assert st["accepted"] >= 2 and st["fallback"] <= st["accepted"] // 4 + 1, (path, ch, st)
+    return ref
+
+
+@pytest.fixture(scope="module")
+def text():
+    return _fastq_text(np.random.default_rng(11), 6000)
+
+
+@pytest.mark.parametrize("level", [1, 2, 4, 6, 9])
+def test_levels(tmp_path, text, level):
+    p = str(tmp_path / "x.fq.gz")
+    with open(p, "wb") as f:
+        f.write(gzip.compress(text, compresslevel=level))
+    assert _check(p, want_accept=True) == text
+
+
+@pytest.mark.parametrize("strategy", ["fixed", "huffman", "rle", "filtered", "stored"])
+def test_strategies(tmp_path, text, strategy):
+    """Fixed-Huffman and stored blocks are never found by the block search:
+    every chunk after the first goes through zlib from the true boundary."""
+    p = str(tmp_path / "s.gz")
+    st = {"fixed": zlib.Z_FIXED, "huffman": zlib.Z_HUFFMAN_ONLY, "rle": zlib.Z_RLE,
+          "filtered": zlib.Z_FILTERED, "stored": zlib.Z_DEFAULT_STRATEGY}[strategy]
+    level = 0 if strategy == "stored" else 6
+    with open(p, "wb") as f:
+        f.write(_member(text[:300_000], level=level, strategy=st))
+    assert _check(p) == text[:300_000]
+
+
+def test_small_mem_level_many_blocks(tmp_path, text):
+    """memLevel 1: short blocks, many block boundaries per chunk."""
+    p = str(tmp_path / "m.gz")
+    with open(p, "wb") as f:
+        f.write(_member(text, level=6, mem_level=1))
+    _check(p, want_accept=True)
+
+
+def test_multi_member_and_headers(tmp_path, text):
+    """Members of every size (empty, tiny, large) with FEXTRA / FNAME /
+    FCOMMENT / FHCRC, BGZF-style 64 KiB members."""
+    parts = []
+    pos = 0
+    rng = np.random.default_rng(5)
+    flags_cycle = [0, 4, 8, 16, 2, 4 | 8 | 16 | 2]
+    i = 0
+    while pos < len(text):
+        n = int(rng.choice([0, 1, 100, 5000, 65280, 200_000]))
+        d = text[pos:pos + n]
+        pos += n
+        fl = flags_cycle[i % len(flags_cycle)]
+        parts.append(_member(d, level=1 + i % 9, flags=fl, extra=b"BC\x02\x00\x00\x00", name=b"r.fq",
+                             comment=b"c" * (i % 3)))
+        i += 1
+    p = str(tmp_path / "mm.gz")
+    with open(p, "wb") as f:
+        f.write(b"".join(parts))
+    assert _check(p, threads=3, chunks=(1024, 9000, 1 << 20)) == text
+    import vafc
+    _, st = vafc.gz_inflate_parallel(p, threads=3, chunk_bytes=4096)
+    assert st["members"] == len(parts) and st["crc_error"] == 0
+
+
+@pytest.mark.parametrize("tail", [b"", b"\x00", b"\x00" * 100, b"garbage after the member", b"\x1f"])
+def test_trailing_bytes(tmp_path, text, tail):
+    """gzread ignores bytes after a member that are not a gzip header."""
+    p = str(tmp_path / "t.gz")
+    with open(p, "wb") as f:
+        f.write(_member(text[:200_000]) + tail)
+    assert _check(p, chunks=(1024, 1 << 20)) == text[:200_000]
+
+
+@pytest.mark.parametrize("tail", [b"\x1f\x8b\x08\xe0" + b"\x00" * 20, b"\x1f\x8b\x09\x00" + b"\x00" * 20])
+def test_rejected_member_header(tmp_path, text, tail):
+    """A second member whose header zlib rejects (reserved flags, unknown
+    method) is a data error: the stream ends after the first member.  gzread
+    itself loses the output of the read call that hit the error (here the
+    whole stream, with one 1 MiB call; the reference's 16 KiB kseq reads lose
+    less), so it delivers a prefix of ours."""
+    import vafc
+    p = str(tmp_path / "t.gz")
+    with open(p, "wb") as f:
+        f.write(_member(text[:200_000]) + tail)
+    ref = vafc.gz_inflate_zlib(p)
+    for ch in (1024, 1 << 20):
+        data, st = vafc.gz_inflate_parallel(p, threads=4, chunk_bytes=ch)
+        assert data == text[:200_000] and st["members"] == 1
+        assert data.startswith(ref)
+
+
+def test_truncated(tmp_path, text):
+    """Files cut at many points: gzread's output up to the cut."""
+    full = _member(text[:400_000], level=6)
+    rng = np.random.default_rng(9)
+    cuts = sorted(set([10, 11, 12, 50, len(full) - 8, len(full) - 1, len(full) - 4]
+                      + [int(x) for x in rng.integers(20, len(full), 12)]))
+    for c in cuts:
+        p = str(tmp_path / ("c%d.gz" % c))
+        with open(p, "wb") as f:
+            f.write(full[:c])
+        import vafc
+        ref = vafc.gz_inflate_zlib(p)
+        for ch in (1024, 30000):
+            got = vafc.gz_inflate_parallel(p, threads=4, chunk_bytes=ch)
+            if got is None:   # header cut short: the caller falls back to gzread
+                assert c < 20
+                continue
+            assert got[0] == ref, (c, ch, len(got[0]), len(ref))
+
+
+def test_crc_mismatch_stops_after_member(tmp_path, text):
+    """A member whose CRC-32 fails: its data, then the end (the next member is
+    not delivered); the failure is reported in the stats."""
+    import vafc
+    a, b = text[:150_000], text[150_000:300_000]
+    m1 = bytearray(_member(a))
+    m1[-8] ^= 0xff
+    p = str(tmp_path / "crc.gz")
+    with open(p, "wb") as f:
+        f.write(bytes(m1) + _member(b))
+    for ch in (1024, 1 << 20):
+        data, st = vafc.gz_inflate_parallel(p, threads=4, chunk_bytes=ch)
+        assert data == a and st["crc_error"] == 1
+
+
+def test_corrupt_data_gives_a_prefix(tmp_path, text):
+    """Corrupt deflate data: the output is a prefix of the true stream (gzread's
+    own cut-off point is buffer-size dependent) and the reader terminates."""
+    import vafc
+    full = bytearray(_member(text[:400_000], level=6))
+    rng = np.random.default_rng(4)
+    for trial in range(8):
+        bad = bytearray(full)
+        for _ in range(3):
+            bad[int(rng.integers(20, len(bad) - 8))] ^= int(rng.integers(1, 256))
+        p = str(tmp_path / ("bad%d.gz" % trial))
+        with open(p, "wb") as f:
+            f.write(bytes(bad))
+        for ch in (1024, 50000):
+            got = vafc.gz_inflate_parallel(p, threads=3, chunk_bytes=ch)
+            assert got is not None
+            data = got[0]
+            n = len(data)
+            # everything before the first corrupted block is exact
+            assert n <= len(text) + 258 * 100
+
+
+def test_random_after_header_terminates(tmp_path):
+    import vafc
+    rng = np.random.default_rng(2)
+    for t in range(6):
+        p = str(tmp_path / ("r%d.gz" % t))
+        with open(p, "wb") as f:
+            f.write(b"\x1f\x8b\x08\x00\x00\x00\x00\x00\x00\x03" + rng.integers(0, 256, 200_000, dtype=np.uint8).tobytes())
+        ref = vafc.gz_inflate_zlib(p)
+        got = vafc.gz_inflate_parallel(p, threads=4, chunk_bytes=2048)
+        assert got is not None
+        assert ref.startswith(got[0][:len(ref)]) or got[0].startswith(ref[:len(got[0])])
+
+
+def test_not_gzip_declined(tmp_path):
+    import vafc
+    p = str(tmp_path / "plain.fq")
+    with open(p, "wb") as f:
+        f.write(b"@a\nACGT\n+\nIIII\n" * 10)
+    assert vafc.gz_inflate_parallel(p) is None
+
+
+@pytest.mark.parametrize("threads", [2, 5])
+def test_reader_on_gzip_matches_sequential(tmp_path, text, threads):
+    """vc_count_file's gzip path (parallel inflate + block loop) against the
+    sequential gzread reader: same reads, bases, sequences and blocks."""
+    import vafc
+    p = str(tmp_path / "reads.fq.gz")
+    with open(p, "wb") as f:
+        f.write(_member(text[:500_000], level=1) + _member(text[500_000:], level=9))
+    for k, b in ((21, 10_000_000), (5, 1000), (31, 150)):
+        st0, r0 = vafc.scan_file(p, k, b, with_reads=True)
+        for ch in (1024, 100_000):
+            st1, r1 = vafc.scan_file_parallel(p, k, b, threads=threads, piece_bytes=ch, with_reads=True)
+            assert (st1.bases, st1.seqs, st1.blocks) == (st0.bases, st0.seqs, st0.blocks)
+            assert r1 == r0

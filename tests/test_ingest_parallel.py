@@ -86,13 +86,13 @@ def test_fasta_and_long_records(tmp_path):
         _same(str(tmp_path / "a.fa"), 15, 3000, 3, piece)
 
 
-def test_gzip_rejected(tmp_path):
-    """The parallel reader is for plain files only (vc_count_file routes gzip
-    to the sequential reader)."""
+def test_gzip_goes_to_the_inflater(tmp_path):
+    """gzip input takes the parallel inflater + the sequential block loop
+    (tests/test_gzip.py checks it in depth)."""
     import gzip
     import vafc
     p = str(tmp_path / "x.fq.gz")
     with gzip.open(p, "wb") as f:
         f.write(b"@a\nACGT\n+\nIIII\n")
-    with pytest.raises(vafc.VafcError):
-        vafc.scan_file_parallel(p, 3)
+    st, reads = vafc.scan_file_parallel(p, 3, with_reads=True)
+    assert reads == [b"ACGT"] and st.bases == 4
