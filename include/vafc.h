@@ -194,6 +194,9 @@ int vc_scan_file_parallel(const char *path, int k, int block_bases, int n_thread
 int64_t vc_gz_inflate_parallel(const char *path, int n_threads, uint64_t chunk_bytes, uint8_t *out,
                                uint64_t cap, uint64_t *stats6);
 int64_t vc_gz_inflate_zlib(const char *path, uint8_t *out, uint64_t cap);
+/* Host-only: zlib-compatible CRC-32 of p[0..n) continuing from crc (the
+ * inflater's member check; PCLMULQDQ folding where the CPU has it). */
+uint32_t vc_gz_crc32(uint32_t crc, const uint8_t *p, uint64_t n);
 
 /* Host-only: the kseq_read return value of every record until -1 (inclusive),
  * written while they fit; returns the number of calls made, or VC_EIO. */

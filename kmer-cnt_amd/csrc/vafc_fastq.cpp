@@ -21,19 +21,13 @@ bool VcFastqReader::open(const char *path, size_t window)
 	return buf_ != nullptr;
 }
 
-// Compressed bytes per inflate chunk of the parallel gzip reader (about
-// 14 MB of FASTQ text at level 6).
-#ifndef VC_GZ_CHUNK_BYTES
-#define VC_GZ_CHUNK_BYTES ((uint64_t)4 << 20)
-#endif
-
 bool VcFastqReader::open_parallel(const char *path, int threads, uint64_t chunk_bytes, size_t window)
 {
 	close();
 	if (threads >= 1) {
-		if (!chunk_bytes) {
+		if (!chunk_bytes) {   // 0: sized by the inflater from the file size
 			const char *e = getenv("VAFC_GZ_CHUNK");   // test knob
-			chunk_bytes = e && atoll(e) > 0 ? (uint64_t)atoll(e) : VC_GZ_CHUNK_BYTES;
+			chunk_bytes = e && atoll(e) > 0 ? (uint64_t)atoll(e) : 0;
 		}
 		gzp_ = vc_gzp_open(path, threads, chunk_bytes);
 	}

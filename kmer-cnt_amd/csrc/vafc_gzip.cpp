@@ -12,6 +12,7 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <immintrin.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -279,64 +280,166 @@ bool read_dynamic(BitIn &in, Tables &T)
 }
 
 // ---------------------------------------------------------------------------
-// speculative output: 16-bit symbols; MARK | i names byte i of the 32 KiB
-// window that precedes the chunk (i = 32768 - distance before the start)
+// speculative output.  Phase 1 writes 16-bit symbols: MARK | i names byte i
+// of the 32 KiB window that precedes the chunk (i = 32768 - distance before
+// the start).  Once the last 32 KiB of symbols hold no marker, no later
+// back-reference can reach one, so phase 2 writes plain bytes: t[] is indexed
+// by output position, its first `res` bytes are filled in later by resolving
+// s[0..res) against the window, the rest are final when written.
 // ---------------------------------------------------------------------------
 struct Out {
-	uint16_t *p = nullptr;
-	size_t n = 0, cap = 0;
-	int64_t floor = -(int64_t)WSIZE;   // lowest index a back-reference may reach
+	uint16_t *s = nullptr;             // phase 1 symbols
+	size_t ns = 0, caps = 0;
+	uint8_t *t = nullptr;              // text by output position (phase 2)
+	size_t nt = 0, capt = 0;
+	bool wide = true;                  // in phase 1
+	size_t res = 0;                    // t[0..res) still to be resolved from s
+	int64_t floor = -(int64_t)WSIZE;   // lowest output index a back-reference may reach
 	uint32_t min_mark = WSIZE;         // lowest window index referenced
-	~Out() { free(p); }
-	bool grow(size_t need)
+	int64_t last_mark = -1;            // highest output index that may hold a marker
+	~Out()
 	{
-		if (need > OUT_CAP + 1024) return false;
-		size_t nc = cap ? cap : ((size_t)1 << 20);
+		free(s);
+		free(t);
+	}
+	size_t total() const { return wide ? ns : nt; }
+	void reset(bool known_history)
+	{
+		ns = nt = res = 0;
+		min_mark = WSIZE;
+		last_mark = -1;
+		floor = known_history ? 0 : -(int64_t)WSIZE;
+		wide = !known_history;
+	}
+	static bool grow_buf(void **p, size_t *cap, size_t need, size_t elem)
+	{
+		if (need > OUT_CAP + 4096) return false;
+		size_t nc = *cap ? *cap : ((size_t)1 << 20);
 		while (nc < need) nc *= 2;
-		uint16_t *q = (uint16_t *)realloc(p, nc * sizeof(uint16_t));
+		void *q = realloc(*p, nc * elem);
 		if (!q) return false;
-		p = q;
-		cap = nc;
+		*p = q;
+		*cap = nc;
+		return true;
+	}
+	bool room(size_t k)
+	{
+		if (wide) return caps - ns >= k || grow_buf((void **)&s, &caps, ns + k, 2);
+		return capt - nt >= k || grow_buf((void **)&t, &capt, nt + k, 1);
+	}
+	// phase 1 -> 2: the last 32 KiB of symbols are literal bytes
+	bool narrow()
+	{
+		if (capt < ns + 600 && !grow_buf((void **)&t, &capt, ns + ((size_t)1 << 20), 1)) return false;
+		const size_t h = ns < WSIZE ? ns : WSIZE;
+		for (size_t i = ns - h; i < ns; ++i) t[i] = (uint8_t)s[i];
+		res = ns - h;
+		nt = ns;
+		wide = false;
+		return true;
+	}
+	// end of chunk: everything not yet in t is resolved later
+	bool finish()
+	{
+		if (!wide) return true;
+		if (capt < ns + 64 && !grow_buf((void **)&t, &capt, ns + 64, 1)) return false;
+		res = ns;
+		nt = ns;
 		return true;
 	}
 };
 
-// One Huffman-coded block body up to its end-of-block code.
-bool decode_huff(BitIn &in, const Tables &T, Out &o)
+inline void copy_match8(uint8_t *dst, unsigned dist, unsigned len)
+{
+	const uint8_t *s = dst - dist;
+	if (dist >= 16) {
+		for (unsigned i = 0; i < len; i += 16) memcpy(dst + i, s + i, 16);
+	} else if (dist >= 8) {
+		for (unsigned i = 0; i < len; i += 8) memcpy(dst + i, s + i, 8);
+	} else if (dist == 1) {
+		memset(dst, s[0], len);
+	} else {
+		for (unsigned i = 0; i < len; ++i) dst[i] = s[i];
+	}
+}
+
+// One Huffman-coded block body up to its end-of-block code.  Returns 1 at
+// the end of the block, 0 on an error, 2 (phase 1 only) when the output has
+// just switched to phase 2 and the block continues there.
+template <bool WIDE>
+int decode_huff(BitIn &in, const Tables &T, Out &o)
 {
 	for (;;) {
-		if (__builtin_expect(o.cap - o.n < 600, 0) && !o.grow(o.n + 600)) return false;
-		if (__builtin_expect(in.pos > in.n + 16, 0)) return false;
+		if (WIDE) {
+			if (__builtin_expect((int64_t)o.ns - o.last_mark > (int64_t)WSIZE, 0)) return o.narrow() ? 2 : 0;
+			if (__builtin_expect(o.caps - o.ns < 600, 0) && !o.room(600)) return 0;
+		} else {
+			if (__builtin_expect(o.capt - o.nt < 600, 0) && !o.room(600)) return 0;
+		}
+		if (__builtin_expect(in.pos > in.n + 16, 0)) return 0;
 		in.refill();
 		uint32_t e = T.lit[in.buf & ((1u << LROOT) - 1)];
 		if (e_kind(e) == K_SUB) e = T.lit[e_val(e) + ((in.buf >> LROOT) & ((1u << e_ext(e)) - 1))];
 		in.drop(e_len(e));
 		if (e_kind(e) == K_LIT) {
-			o.p[o.n++] = (uint16_t)e_val(e);
+			size_t n = WIDE ? o.ns : o.nt;
+			if (WIDE) o.s[n++] = (uint16_t)e_val(e);
+			else o.t[n++] = (uint8_t)e_val(e);
 			// up to two more literals without a refill (56 - 15 >= 2 x 15 + 11)
 			uint32_t e2 = T.lit[in.buf & ((1u << LROOT) - 1)];
-			if (e_kind(e2) != K_LIT) continue;
-			in.drop(e_len(e2));
-			o.p[o.n++] = (uint16_t)e_val(e2);
-			e2 = T.lit[in.buf & ((1u << LROOT) - 1)];
-			if (e_kind(e2) != K_LIT) continue;
-			in.drop(e_len(e2));
-			o.p[o.n++] = (uint16_t)e_val(e2);
+			if (e_kind(e2) == K_LIT) {
+				in.drop(e_len(e2));
+				if (WIDE) o.s[n++] = (uint16_t)e_val(e2);
+				else o.t[n++] = (uint8_t)e_val(e2);
+				e2 = T.lit[in.buf & ((1u << LROOT) - 1)];
+				if (e_kind(e2) == K_LIT) {
+					in.drop(e_len(e2));
+					if (WIDE) o.s[n++] = (uint16_t)e_val(e2);
+					else o.t[n++] = (uint8_t)e_val(e2);
+				}
+			}
+			if (WIDE) o.ns = n;
+			else o.nt = n;
 			continue;
 		}
-		if (e_kind(e) == K_EOB) return !in.overrun();
-		if (e_kind(e) != K_LEN) return false;
+		if (e_kind(e) == K_EOB) return in.overrun() ? 0 : 1;
+		if (e_kind(e) != K_LEN) return 0;
 		const unsigned len = e_val(e) + in.take(e_ext(e));
 		uint32_t d = T.dist[in.buf & ((1u << DROOT) - 1)];
 		if (e_kind(d) == K_SUB) d = T.dist[e_val(d) + ((in.buf >> DROOT) & ((1u << e_ext(d)) - 1))];
-		if (e_kind(d) == K_BAD) return false;
+		if (e_kind(d) == K_BAD) return 0;
 		in.drop(e_len(d));
 		const unsigned dist = e_val(d) + in.take(e_ext(d));
-		const int64_t src = (int64_t)o.n - (int64_t)dist;
-		uint16_t *dst = o.p + o.n;
+		if (!WIDE) {   // every source byte lies in t[nt - 32768, nt): literal text
+			if ((int64_t)o.nt - (int64_t)dist < o.floor) return 0;
+			copy_match8(o.t + o.nt, dist, len);
+			o.nt += len;
+			continue;
+		}
+		const int64_t src = (int64_t)o.ns - (int64_t)dist;
+		uint16_t *dst = o.s + o.ns;
 		if (src >= 0) {
 			const uint16_t *s = dst - dist;
-			if (dist >= 8) {
+			if (src <= o.last_mark) {   // the source may hold markers: copy and look
+				uint64_t acc = 0;
+				if (dist >= 8) {   // (the look may see up to 7 symbols past the source: harmless)
+					for (unsigned i = 0; i < len; i += 8) {
+						uint64_t a, b;
+						memcpy(&a, s + i, 8);
+						memcpy(&b, s + i + 4, 8);
+						memcpy(dst + i, &a, 8);
+						memcpy(dst + i + 4, &b, 8);
+						acc |= a | b;
+					}
+				} else {
+					for (unsigned i = 0; i < len; ++i) {
+						const uint16_t v = s[i];
+						dst[i] = v;
+						acc |= v;
+					}
+				}
+				if (acc & 0x8000800080008000ull) o.last_mark = (int64_t)o.ns + len - 1;
+			} else if (dist >= 8) {
 				for (unsigned i = 0; i < len; i += 8) memcpy(dst + i, s + i, 16);
 			} else if (dist == 1) {
 				const uint16_t v = s[0];
@@ -345,16 +448,26 @@ bool decode_huff(BitIn &in, const Tables &T, Out &o)
 				for (unsigned i = 0; i < len; ++i) dst[i] = s[i];
 			}
 		} else {
-			if (src < o.floor) return false;   // before the member's first byte
+			if (src < o.floor) return 0;   // before the member's first byte
 			const uint32_t m = (uint32_t)(src + WSIZE);
 			if (m < o.min_mark) o.min_mark = m;
 			for (unsigned i = 0; i < len; ++i) {
 				const int64_t si = src + (int64_t)i;
-				dst[i] = si < 0 ? (uint16_t)(MARK | (uint32_t)(si + WSIZE)) : o.p[si];
+				dst[i] = si < 0 ? (uint16_t)(MARK | (uint32_t)(si + WSIZE)) : o.s[si];
 			}
+			o.last_mark = (int64_t)o.ns + len - 1;
 		}
-		o.n += len;
+		o.ns += len;
 	}
+}
+
+int decode_huff_any(BitIn &in, const Tables &T, Out &o)
+{
+	if (o.wide) {
+		const int r = decode_huff<true>(in, T, o);
+		if (r != 2) return r;
+	}
+	return decode_huff<false>(in, T, o);
 }
 
 // Stored block body; the 3 header bits are consumed.
@@ -364,10 +477,15 @@ bool decode_stored(BitIn &in, Out &o)
 	if (byte + 4 > in.n) return false;
 	const unsigned len = in.p[byte] | in.p[byte + 1] << 8, nlen = in.p[byte + 2] | in.p[byte + 3] << 8;
 	if (len != (~nlen & 0xffffu) || byte + 4 + len > in.n) return false;
-	if (o.cap - o.n < (size_t)len + 600 && !o.grow(o.n + len + 600)) return false;
+	if (!o.room((size_t)len + 600)) return false;
 	const uint8_t *s = in.p + byte + 4;
-	for (unsigned i = 0; i < len; ++i) o.p[o.n + i] = s[i];
-	o.n += len;
+	if (o.wide) {
+		for (unsigned i = 0; i < len; ++i) o.s[o.ns + i] = s[i];
+		o.ns += len;
+	} else {
+		memcpy(o.t + o.nt, s, len);
+		o.nt += len;
+	}
 	in.init(in.p, in.n, (byte + 4 + len) * 8);
 	return true;
 }
@@ -421,6 +539,28 @@ struct Chunk {
 	std::unique_ptr<Tables> tab{new Tables};
 };
 
+// After a final block: the member trailer, then the next member's header.
+// Returns 1 to go on decoding at *in, 0 at the end of the stream, -1 on an
+// error.
+int member_end(const uint8_t *p, uint64_t n, BitIn &in, Chunk &C)
+{
+	Out &o = C.out;
+	uint64_t byte = (in.bitpos() + 7) >> 3;
+	if (byte + 8 > n) return -1;
+	C.events.push_back({o.total(), le32(p + byte), le32(p + byte + 4)});
+	byte += 8;
+	if (n - byte < 2 || p[byte] != 0x1f || p[byte + 1] != 0x8b) {   // end, or trailing garbage
+		C.stream_end = true;
+		C.end = byte * 8;
+		return 0;
+	}
+	const int64_t d = member_header(p, n, byte);
+	if (d < 0) return -1;
+	o.floor = (int64_t)o.total();
+	in.init(p, n, (uint64_t)d * 8);
+	return 1;
+}
+
 bool decode_blocks(const uint8_t *p, uint64_t n, BitIn &in, Chunk &C, bool first_checked)
 {
 	Out &o = C.out;
@@ -429,56 +569,72 @@ bool decode_blocks(const uint8_t *p, uint64_t n, BitIn &in, Chunk &C, bool first
 		const uint64_t at = in.bitpos();
 		if (at >= C.nom_b && !first) {
 			C.end = at;
-			return true;
+			return o.finish();
 		}
 		first = false;
 		in.refill();
 		const unsigned bfinal = in.take(1), btype = in.take(2);
 		bool good;
 		if (btype == 0) good = decode_stored(in, o);
-		else if (btype == 1) good = decode_huff(in, fixed_tables(), o);
-		else if (btype == 2) good = read_dynamic(in, *C.tab) && decode_huff(in, *C.tab, o);
+		else if (btype == 1) good = decode_huff_any(in, fixed_tables(), o) == 1;
+		else if (btype == 2) good = read_dynamic(in, *C.tab) && decode_huff_any(in, *C.tab, o) == 1;
 		else good = false;
 		if (!good) return false;
 		if (!bfinal) continue;
-		uint64_t byte = (in.bitpos() + 7) >> 3;
-		if (byte + 8 > n) return false;
-		C.events.push_back({o.n, le32(p + byte), le32(p + byte + 4)});
-		byte += 8;
-		if (n - byte < 2 || p[byte] != 0x1f || p[byte + 1] != 0x8b) {   // end, or trailing garbage
-			C.stream_end = true;
-			C.end = byte * 8;
-			return true;
-		}
-		const int64_t d = member_header(p, n, byte);
-		if (d < 0) return false;
-		o.floor = (int64_t)o.n;
-		in.init(p, n, (uint64_t)d * 8);
+		const int r = member_end(p, n, in, C);
+		if (r < 0) return false;
+		if (r == 0) return o.finish();
 	}
 }
 
-// Cheap tests on a candidate dynamic block header at bit b: block type,
-// symbol counts and a complete code-length code.
-inline bool quick_dynamic(const uint8_t *p, uint64_t n, uint64_t b)
+// First 13 header bits that can start a dynamic block: BTYPE = 2, at most
+// 286 literal/length and 30 distance codes (about 22 % of patterns).
+const uint8_t *head13()
 {
-	const uint64_t byte = b >> 3;
-	if (byte + 8 > n) return false;
-	uint64_t w;
-	memcpy(&w, p + byte, 8);
-	w >>= (b & 7);
-	if ((w & 6) != 4) return false;
-	if (((w >> 3) & 31) > 29 || ((w >> 8) & 31) > 29) return false;
+	static uint8_t *t = [] {
+		uint8_t *x = new uint8_t[8192];
+		for (unsigned w = 0; w < 8192; ++w) x[w] = (w & 6) == 4 && ((w >> 3) & 31) <= 29 && ((w >> 8) & 31) <= 29;
+		return x;
+	}();
+	return t;
+}
+
+// Cheap tests on a candidate dynamic block header at bit b (whose first 13
+// bits passed head13): a complete code-length code.
+// Kraft sum (in units of 2^-7) of four 3-bit code lengths
+const uint16_t *kraft4()
+{
+	static uint16_t *t = [] {
+		uint16_t *x = new uint16_t[4096];
+		for (unsigned w = 0; w < 4096; ++w) {
+			unsigned k = 0;
+			for (int i = 0; i < 4; ++i) {
+				const unsigned l = (w >> (3 * i)) & 7;
+				if (l) k += 128u >> l;
+			}
+			x[w] = (uint16_t)k;
+		}
+		return x;
+	}();
+	return t;
+}
+
+inline bool quick_dynamic(const uint8_t *p, uint64_t n, uint64_t b, uint64_t w)
+{
 	const unsigned hclen = (unsigned)((w >> 13) & 15) + 4;
 	const uint64_t b2 = b + 17, byte2 = b2 >> 3;
 	if (byte2 + 8 > n) return false;
 	uint64_t w2;
 	memcpy(&w2, p + byte2, 8);
 	w2 >>= (b2 & 7);
-	unsigned kraft = 0;
-	for (unsigned i = 0; i < hclen; ++i) {
-		const unsigned l = (unsigned)(w2 >> (3 * i)) & 7;
-		if (l) kraft += 128u >> l;
-	}
+	// the code-length code: hclen 3-bit lengths, which must form a complete code
+	w2 &= hclen == 19 ? ~0ull >> 7 : ((1ull << (3 * hclen)) - 1);
+	const uint16_t *K = kraft4();
+	unsigned kraft = K[w2 & 4095];
+	if (kraft > 128) return false;
+	kraft += K[(w2 >> 12) & 4095];
+	if (kraft > 128) return false;
+	kraft += K[(w2 >> 24) & 4095] + K[(w2 >> 36) & 4095] + K[(w2 >> 48) & 511];
 	return kraft == 128;
 }
 
@@ -506,11 +662,9 @@ void decode_chunk(const uint8_t *p, uint64_t n, uint64_t first_bit, Chunk &C)
 	C.start = -1;
 	C.events.clear();
 	Out &o = C.out;
-	o.n = 0;
-	o.min_mark = WSIZE;
 	BitIn in;
 	if (C.index == 0) {   // the stream's start: known (empty) history
-		o.floor = 0;
+		o.reset(true);
 		C.start = (int64_t)first_bit;
 		in.init(p, n, first_bit);
 		C.ok = decode_blocks(p, n, in, C, true);
@@ -519,15 +673,22 @@ void decode_chunk(const uint8_t *p, uint64_t n, uint64_t first_bit, Chunk &C)
 	const uint64_t lim = std::min(C.nom_b, n * 8);
 	Tables scratch;
 	const double t0 = gz_now();
+	const uint8_t *H = head13();
+	uint64_t w8 = 0, wbyte = ~0ull;
 	for (uint64_t b = C.nom_a; b < lim; ++b) {
-		if (!quick_dynamic(p, n, b)) continue;
-		o.n = 0;
-		o.floor = -(int64_t)WSIZE;
-		o.min_mark = WSIZE;
+		const uint64_t byte = b >> 3;
+		if (byte + 24 > n) break;   // (a block start this close to the end is left to zlib)
+		if (byte != wbyte) {   // one load serves the 8 bit offsets of a byte
+			memcpy(&w8, p + byte, 8);
+			wbyte = byte;
+		}
+		const uint64_t w = w8 >> (b & 7);
+		if (!H[w & 8191] || !quick_dynamic(p, n, b, w)) continue;
+		o.reset(false);
 		C.events.clear();
 		in.init(p, n, b);
 		in.take(3);
-		if (!read_dynamic(in, *C.tab) || !decode_huff(in, *C.tab, o)) continue;
+		if (!read_dynamic(in, *C.tab) || decode_huff_any(in, *C.tab, o) != 1) continue;
 		// the candidate block decoded; its header bit said whether it was final
 		BitIn h;
 		h.init(p, n, b);
@@ -541,20 +702,12 @@ void decode_chunk(const uint8_t *p, uint64_t n, uint64_t first_bit, Chunk &C)
 			~Acc() { prof_decode_us += (uint64_t)((gz_now() - t) * 1e6); }
 		} acc{t1};
 		if (final_blk) {   // continue through the trailer like decode_blocks
-			uint64_t byte = (in.bitpos() + 7) >> 3;
-			if (byte + 8 > n) return;
-			C.events.push_back({o.n, le32(p + byte), le32(p + byte + 4)});
-			byte += 8;
-			if (n - byte < 2 || p[byte] != 0x1f || p[byte + 1] != 0x8b) {
-				C.stream_end = true;
-				C.end = byte * 8;
-				C.ok = true;
+			const int r = member_end(p, n, in, C);
+			if (r < 0) return;
+			if (r == 0) {
+				C.ok = o.finish();
 				return;
 			}
-			const int64_t d = member_header(p, n, byte);
-			if (d < 0) return;
-			o.floor = (int64_t)o.n;
-			in.init(p, n, (uint64_t)d * 8);
 		}
 		C.ok = decode_blocks(p, n, in, C, false);
 		return;
@@ -565,7 +718,7 @@ void decode_chunk(const uint8_t *p, uint64_t n, uint64_t first_bit, Chunk &C)
 // resolved output handed to the reader
 // ---------------------------------------------------------------------------
 struct Piece {
-	uint8_t *text = nullptr;
+	uint8_t *text = nullptr;          // owned (malloc); an accepted chunk's t[] is swapped in
 	size_t n = 0, cap = 0;
 	Chunk *src = nullptr;             // symbols still to resolve (accepted chunk)
 	std::vector<uint8_t> window;      // the 32 KiB before src's first symbol
@@ -585,13 +738,20 @@ struct Piece {
 	}
 };
 
+// t[0..res) of the source chunk from its symbols and the window; then the
+// chunk's text buffer becomes the piece's (the piece's old buffer goes back
+// to the chunk for reuse).
 void resolve(Piece &P)
 {
-	const Chunk &C = *P.src;
-	const uint16_t *s = C.out.p;
-	const size_t n = C.out.n;
-	uint8_t *t = P.text;
-	const uint8_t *w = P.window.data();
+	Out &o = P.src->out;
+	const uint16_t *s = o.s;
+	uint8_t *t = o.t;
+	const size_t n = o.res;
+	// symbol -> byte: literals map to themselves, MARK | i to window byte i
+	static thread_local std::unique_ptr<uint8_t[]> lut(new uint8_t[65536]);
+	uint8_t *L = lut.get();
+	for (int v = 0; v < 256; ++v) L[v] = (uint8_t)v;
+	memcpy(L + MARK, P.window.data(), WSIZE);
 	size_t i = 0;
 	for (; i + 32 <= n; i += 32) {
 		uint16_t acc = 0;
@@ -599,14 +759,98 @@ void resolve(Piece &P)
 		if (acc < 256) {
 			for (int k = 0; k < 32; ++k) t[i + k] = (uint8_t)s[i + k];
 		} else {
-			for (int k = 0; k < 32; ++k) {
-				const uint16_t v = s[i + k];
-				t[i + k] = v < 256 ? (uint8_t)v : w[v & (WSIZE - 1)];
-			}
+			for (int k = 0; k < 32; ++k) t[i + k] = L[s[i + k]];
 		}
 	}
-	for (; i < n; ++i) t[i] = s[i] < 256 ? (uint8_t)s[i] : w[s[i] & (WSIZE - 1)];
-	P.n = n;
+	for (; i < n; ++i) t[i] = L[s[i]];
+	std::swap(P.text, o.t);
+	std::swap(P.cap, o.capt);
+	P.n = o.nt;
+}
+
+// CRC-32 (gzip's, zlib's crc32) by carry-less multiplication: four 128-bit
+// lanes folded over 64-byte blocks, then one lane, then Barrett reduction
+// (Gopal et al., "Fast CRC Computation for Generic Polynomials Using PCLMULQDQ
+// Instruction", Intel 2009; bit-reflected constants from its appendix).
+// Pre- and post-inverted like zlib's; len a multiple of 16, at least 64.
+__attribute__((target("pclmul,sse4.1"))) inline __m128i fold128(__m128i a, __m128i b, __m128i k)
+{
+	return _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(a, k, 0x11), b), _mm_clmulepi64_si128(a, k, 0x00));
+}
+
+__attribute__((target("pclmul,sse4.1"))) uint32_t crc32_fold(uint32_t crc, const uint8_t *buf, uint64_t len)
+{
+	alignas(16) static const uint64_t k1k2[] = {0x0154442bd4ull, 0x01c6e41596ull};
+	alignas(16) static const uint64_t k3k4[] = {0x01751997d0ull, 0x00ccaa009eull};
+	alignas(16) static const uint64_t k5k0[] = {0x0163cd6124ull, 0};
+	alignas(16) static const uint64_t poly[] = {0x01db710641ull, 0x01f7011641ull};
+	crc = ~crc;
+	__m128i x1 = _mm_loadu_si128((const __m128i *)(buf + 0x00));
+	__m128i x2 = _mm_loadu_si128((const __m128i *)(buf + 0x10));
+	__m128i x3 = _mm_loadu_si128((const __m128i *)(buf + 0x20));
+	__m128i x4 = _mm_loadu_si128((const __m128i *)(buf + 0x30));
+	x1 = _mm_xor_si128(x1, _mm_cvtsi32_si128((int)crc));
+	__m128i x0 = _mm_load_si128((const __m128i *)k1k2);
+	buf += 64;
+	len -= 64;
+	while (len >= 64) {
+		const __m128i x5 = _mm_clmulepi64_si128(x1, x0, 0x00), x6 = _mm_clmulepi64_si128(x2, x0, 0x00);
+		const __m128i x7 = _mm_clmulepi64_si128(x3, x0, 0x00), x8 = _mm_clmulepi64_si128(x4, x0, 0x00);
+		x1 = _mm_clmulepi64_si128(x1, x0, 0x11);
+		x2 = _mm_clmulepi64_si128(x2, x0, 0x11);
+		x3 = _mm_clmulepi64_si128(x3, x0, 0x11);
+		x4 = _mm_clmulepi64_si128(x4, x0, 0x11);
+		x1 = _mm_xor_si128(_mm_xor_si128(x1, x5), _mm_loadu_si128((const __m128i *)(buf + 0x00)));
+		x2 = _mm_xor_si128(_mm_xor_si128(x2, x6), _mm_loadu_si128((const __m128i *)(buf + 0x10)));
+		x3 = _mm_xor_si128(_mm_xor_si128(x3, x7), _mm_loadu_si128((const __m128i *)(buf + 0x20)));
+		x4 = _mm_xor_si128(_mm_xor_si128(x4, x8), _mm_loadu_si128((const __m128i *)(buf + 0x30)));
+		buf += 64;
+		len -= 64;
+	}
+	x0 = _mm_load_si128((const __m128i *)k3k4);
+	x1 = fold128(x1, x2, x0);
+	x1 = fold128(x1, x3, x0);
+	x1 = fold128(x1, x4, x0);
+	while (len >= 16) {
+		x1 = fold128(x1, _mm_loadu_si128((const __m128i *)buf), x0);
+		buf += 16;
+		len -= 16;
+	}
+	// 128 -> 64 bits
+	x2 = _mm_clmulepi64_si128(x1, x0, 0x10);
+	x3 = _mm_setr_epi32(~0, 0, ~0, 0);
+	x1 = _mm_xor_si128(_mm_srli_si128(x1, 8), x2);
+	x0 = _mm_loadl_epi64((const __m128i *)k5k0);
+	x2 = _mm_srli_si128(x1, 4);
+	x1 = _mm_and_si128(x1, x3);
+	x1 = _mm_xor_si128(_mm_clmulepi64_si128(x1, x0, 0x00), x2);
+	// Barrett reduction to 32 bits
+	x0 = _mm_load_si128((const __m128i *)poly);
+	x2 = _mm_and_si128(x1, x3);
+	x2 = _mm_clmulepi64_si128(x2, x0, 0x10);
+	x2 = _mm_and_si128(x2, x3);
+	x2 = _mm_clmulepi64_si128(x2, x0, 0x00);
+	x1 = _mm_xor_si128(x1, x2);
+	return ~(uint32_t)_mm_extract_epi32(x1, 1);
+}
+
+const bool have_clmul = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+
+uint32_t vc_crc32(uint32_t c, const uint8_t *p, uint64_t n)
+{
+	if (have_clmul && n >= 64) {
+		const uint64_t m = n & ~(uint64_t)15;
+		c = crc32_fold(c, p, m);
+		p += m;
+		n -= m;
+	}
+	while (n) {   // zlib's length is 32-bit
+		const uint64_t m = std::min<uint64_t>(n, (uint64_t)1 << 30);
+		c = (uint32_t)crc32(c, p, (uInt)m);
+		p += m;
+		n -= m;
+	}
+	return c;
 }
 
 void piece_crcs(Piece &P)
@@ -614,16 +858,10 @@ void piece_crcs(Piece &P)
 	P.seg_crc.clear();
 	uint64_t a = 0;
 	for (const Event &e : P.events) {
-		P.seg_crc.push_back((uint32_t)crc32(0, P.text + a, (uInt)(e.off - a)));
+		P.seg_crc.push_back(vc_crc32(0, P.text + a, e.off - a));
 		a = e.off;
 	}
-	uint32_t c = 0;
-	for (uint64_t x = a; x < P.n;) {   // crc32's length is 32-bit
-		const uint64_t m = std::min<uint64_t>(P.n - x, (uint64_t)1 << 30);
-		c = (uint32_t)crc32(c, P.text + x, (uInt)m);
-		x += m;
-	}
-	P.seg_crc.push_back(c);
+	P.seg_crc.push_back(vc_crc32(0, P.text + a, P.n - a));
 }
 
 } // namespace
@@ -738,8 +976,8 @@ void VcGzParallel::worker()
 		if (task) {
 			task->resolving = true;
 			lk.unlock();
-			bool ok = task->reserve(task->src->out.n + 64);
-			if (ok) {
+			const bool ok = true;
+			{
 				const double r0 = gz_now();
 				resolve(*task);
 				const double r1 = gz_now();
@@ -910,13 +1148,18 @@ void VcGzParallel::sequencer()
 			P->events = C->events;
 			P->stream_end = C->stream_end;
 			// the window after this chunk: its last 32 KiB, markers resolved
-			const uint16_t *s = C->out.p;
-			const size_t n = C->out.n;
+			const Out &o = C->out;
+			const size_t n = o.nt;
 			uint8_t tail[WSIZE];
 			const size_t tn = std::min<size_t>(n, WSIZE);
 			for (size_t i = 0; i < tn; ++i) {
-				const uint16_t v = s[n - tn + i];
-				tail[i] = v < 256 ? (uint8_t)v : window_[v & (WSIZE - 1)];
+				const size_t x = n - tn + i;
+				if (x >= o.res) {
+					tail[i] = o.t[x];
+				} else {
+					const uint16_t v = o.s[x];
+					tail[i] = v < 256 ? (uint8_t)v : window_[v & (WSIZE - 1)];
+				}
 			}
 			window_append(tail, tn);
 			member_text_ = C->events.empty() ? member_text_ + n : n - C->events.back().off;
@@ -956,6 +1199,11 @@ bool VcGzParallel::start(const char *path, int threads, uint64_t chunk_bytes)
 	const int64_t d = member_header(p_, n_, 0);
 	if (d < 0) return false;
 	first_bit_ = (uint64_t)d * 8;
+	if (threads < 1) threads = 1;
+	if (chunk_bytes == 0) {   // about four chunks per worker, 1..4 MiB each
+		chunk_bytes = n_ / (4 * (uint64_t)threads);
+		chunk_bytes = std::max<uint64_t>((uint64_t)1 << 20, std::min<uint64_t>((uint64_t)4 << 20, chunk_bytes));
+	}
 	if (chunk_bytes < 1024) chunk_bytes = 1024;
 	chunk_bits_ = chunk_bytes * 8;
 	nchunks_ = (n_ * 8 - first_bit_ + chunk_bits_ - 1) / chunk_bits_;
@@ -1104,3 +1352,5 @@ extern "C" int64_t vc_gz_inflate_zlib(const char *path, uint8_t *out, uint64_t c
 	gzclose(f);
 	return (int64_t)tot;
 }
+
+extern "C" uint32_t vc_gz_crc32(uint32_t crc, const uint8_t *p, uint64_t n) { return vc_crc32(crc, p, n); }

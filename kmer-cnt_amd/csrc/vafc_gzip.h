@@ -46,7 +46,8 @@ struct VcGzStats {
 class VcGzParallel;
 
 // nullptr if the file is not gzip, its first header is not one zlib accepts,
-// or it cannot be mapped: the caller then reads it with gzread.
+// or it cannot be mapped: the caller then reads it with gzread.  chunk_bytes
+// 0: about four chunks per worker, 1 to 4 MiB of compressed input each.
 VcGzParallel *vc_gzp_open(const char *path, int threads, uint64_t chunk_bytes);
 // Next bytes of the decompressed stream, in order: > 0 bytes, 0 at the end.
 int64_t vc_gzp_read(VcGzParallel *g, uint8_t *dst, size_t n);

@@ -37,7 +37,7 @@ EXPORTS = (
     "vc_count_block", "vc_count_device", "vc_finish", "vc_reset", "vc_device_counts",
     "vc_bind_outputs", "vc_device_tally", "vc_stream", "vc_set_timing", "vc_kernel_ms",
     "vc_table_info", "vc_count_file", "vc_scan_file", "vc_scan_file_parallel", "vc_scan_records", "vc_reserve_file_ingest",
-    "vc_gz_inflate_parallel", "vc_gz_inflate_zlib",
+    "vc_gz_inflate_parallel", "vc_gz_inflate_zlib", "vc_gz_crc32",
     "vc_fasta_load", "vc_fasta_count", "vc_fasta_name", "vc_fasta_seq", "vc_fasta_data", "vc_fasta_free",
     "vc_count_candidates", "vc_set_nt4_decode",
     "vc_synth_reads",
@@ -112,6 +112,7 @@ def lib():
         "vc_scan_records": (C.c_int64, [C.c_char_p, P, C.c_int64]),
         "vc_gz_inflate_parallel": (C.c_int64, [C.c_char_p, C.c_int, C.c_uint64, P, C.c_uint64, P]),
         "vc_gz_inflate_zlib": (C.c_int64, [C.c_char_p, P, C.c_uint64]),
+        "vc_gz_crc32": (C.c_uint32, [C.c_uint32, P, C.c_uint64]),
         "vc_reserve_file_ingest": (C.c_int, [P, C.c_int]),
         "vc_fasta_load": (C.c_int, [C.c_char_p, C.POINTER(P)]),
         "vc_fasta_count": (C.c_int, [P]),

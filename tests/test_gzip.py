@@ -231,3 +231,16 @@ def test_reader_on_gzip_matches_sequential(tmp_path, text, threads):
             st1, r1 = vafc.scan_file_parallel(p, k, b, threads=threads, piece_bytes=ch, with_reads=True)
             assert (st1.bases, st1.seqs, st1.blocks) == (st0.bases, st0.seqs, st0.blocks)
             assert r1 == r0
+
+
+def test_crc32_matches_zlib():
+    """The member check's CRC-32 (carry-less-multiply folding) against zlib's
+    for every length 0..300, longer buffers and arbitrary starting values."""
+    import ctypes
+    import vafc
+    rng = np.random.default_rng(1)
+    for n in list(range(0, 300)) + [1000, 4095, 4096, 65537, (1 << 20) + 3]:
+        a = rng.integers(0, 256, n, dtype=np.uint8)
+        init = int(rng.integers(0, 2 ** 32))
+        got = vafc.lib().vc_gz_crc32(init, a.ctypes.data_as(ctypes.c_void_p), n)
+        assert got == zlib.crc32(a.tobytes(), init), n
