@@ -32,12 +32,12 @@ bool VcFastqReader::open_parallel(const char *path, int threads, uint64_t chunk_
 		gzp_ = vc_gzp_open(path, threads, chunk_bytes);
 	}
 	if (!gzp_) return open(path, window);
-	cap_ = window;
-	buf_ = (uint8_t *)malloc(cap_);
+	cap_ = 0;
+	buf_ = nullptr;   // points into the inflater's pieces (not owned)
 	b_ = e_ = 0;
 	eof_ = false;
 	hdr_ = 0;
-	return buf_ != nullptr;
+	return true;
 }
 
 bool VcFastqReader::open_fd(int fd, uint64_t off, size_t window)
@@ -57,7 +57,10 @@ void VcFastqReader::close()
 {
 	if (fp_) gzclose(fp_);
 	fp_ = nullptr;
-	if (gzp_) vc_gzp_close(gzp_);
+	if (gzp_) {
+		vc_gzp_close(gzp_);
+		buf_ = nullptr;   // not owned
+	}
 	gzp_ = nullptr;
 	fd_ = -1;
 	free(buf_);
@@ -72,8 +75,15 @@ bool VcFastqReader::refill()
 		do n = pread(fd_, buf_, cap_, (off_t)foff_); while (n < 0 && errno == EINTR);
 		base_ = foff_;
 		if (n > 0) foff_ += (uint64_t)n;
-	} else if (gzp_) {
-		n = (ssize_t)vc_gzp_read(gzp_, buf_, cap_);
+	} else if (gzp_) {   // the inflater's own buffer, no copy
+		const uint8_t *q = nullptr;
+		n = (ssize_t)vc_gzp_span(gzp_, &q, (size_t)1 << 30);
+		if (n > 0) {
+			buf_ = (uint8_t *)q;
+			b_ = 0;
+			e_ = (size_t)n;
+			return true;
+		}
 	} else {
 		n = gzread(fp_, buf_, (unsigned)cap_);
 	}
@@ -123,6 +133,37 @@ int VcFastqReader::line(VcByteBuf *dst)
 	return (int)dst->l;
 }
 
+// line() for the quality string, of which only the length matters: the
+// length and the number of trailing '\r' of the accumulated string are kept
+// instead of its bytes, with the same CR rule (kseq.h:146).
+int VcFastqReader::qual_line(size_t *l, size_t *tcr)
+{
+	if (at_end()) return -1;
+	for (;;) {
+		const uint8_t *p = buf_ + b_;
+		const size_t n = e_ - b_;
+		const uint8_t *nl = (const uint8_t *)memchr(p, '\n', n);
+		const size_t seg = nl ? (size_t)(nl - p) : n;
+		if (seg) {
+			size_t t = 0;
+			while (t < seg && p[seg - 1 - t] == '\r') ++t;
+			*tcr = t == seg ? *tcr + t : t;
+			*l += seg;
+		}
+		if (nl) {
+			b_ += seg + 1;
+			break;
+		}
+		b_ = e_;
+		if (!refill()) break;
+	}
+	if (*l > 1 && *tcr > 0) {
+		--*l;
+		--*tcr;
+	}
+	return (int)*l;
+}
+
 // Name token: up to an isspace() byte (KS_SEP_SPACE); the delimiter (or 0 at
 // end of input) is returned through delim.
 int VcFastqReader::token(int *delim)
@@ -160,7 +201,7 @@ int VcFastqReader::next()
 {
 	int c, d;
 	if (!hdr_ && peek_header() < 0) return -1;   // scan to a '>' or '@' (kseq.h:197-201)
-	seq_.l = qual_.l = name_.l = 0;
+	seq_.l = name_.l = 0;
 	if (token(&d) < 0) return -1;
 	if (d != '\n' && !at_end()) skip_line();          // comment (kseq.h:204)
 	// sequence lines until a line starts with '+', '>' or '@' (kseq.h:209-213)
@@ -176,7 +217,8 @@ int VcFastqReader::next()
 	if (c != '+') return (int)seq_.l;                 // FASTA
 	do c = getc_(); while (c != -1 && c != '\n');     // rest of the '+' line
 	if (c == -1) return -2;
-	while (line(&qual_) >= 0 && qual_.l < seq_.l) {}
+	size_t ql = 0, qcr = 0;
+	while (qual_line(&ql, &qcr) >= 0 && ql < seq_.l) {}
 	hdr_ = 0;
-	return seq_.l == qual_.l ? (int)seq_.l : -2;
+	return seq_.l == ql ? (int)seq_.l : -2;
 }

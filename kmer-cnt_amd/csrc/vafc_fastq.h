@@ -78,7 +78,7 @@ private:
 	bool eof_ = false;
 	int hdr_ = 0;                 // header char already consumed, 0 if none
 	uint64_t hdr_pos_ = 0;        // its file offset (pread source)
-	VcByteBuf seq_, qual_, name_;
+	VcByteBuf seq_, name_;
 	bool keep_name_ = false;
 
 	bool refill();
@@ -90,6 +90,7 @@ private:
 	inline uint64_t last_pos() const { return base_ + b_ - 1; }   // of the byte getc_ just returned
 	inline bool at_end() { return b_ >= e_ && !refill(); }
 	int line(VcByteBuf *dst);     // rest of a line, appended; CR rule on the whole string
+	int qual_line(size_t *l, size_t *tcr);   // the same for a string kept as its length only
 	int token(int *delim);        // up to an isspace() byte, discarded
 	void skip_line();
 };

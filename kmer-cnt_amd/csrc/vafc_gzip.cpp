@@ -871,6 +871,7 @@ public:
 	~VcGzParallel() { shutdown(); }
 	bool start(const char *path, int threads, uint64_t chunk_bytes);
 	int64_t read(uint8_t *dst, size_t n);
+	int64_t span(const uint8_t **out, size_t maxn);
 	void get_stats(VcGzStats *st)
 	{
 		std::lock_guard<std::mutex> lk(mu_);
@@ -900,6 +901,7 @@ private:
 	// reader state
 	Piece *cur_ = nullptr;
 	size_t rd_ = 0, ev_ = 0, seg_a_ = 0;
+	bool spent_ = false;              // cur_ fully read (released at the next span)
 	uint32_t mcrc_ = 0;
 	uint64_t mlen_ = 0;
 	bool done_ = false;
@@ -1219,28 +1221,47 @@ bool VcGzParallel::start(const char *path, int threads, uint64_t chunk_bytes)
 	return true;
 }
 
-int64_t VcGzParallel::read(uint8_t *dst, size_t n)
+// The next bytes of the stream without a copy: *out points into the current
+// piece, valid until the next call (the piece is released then).
+int64_t VcGzParallel::span(const uint8_t **out, size_t maxn)
 {
-	size_t got = 0;
-	while (got < n && !done_) {
+	for (;;) {
+		if (done_ || maxn == 0) return 0;
+		if (cur_ && spent_) {   // release the piece the previous span pointed into
+			const bool last = cur_->stream_end;
+			{
+				std::lock_guard<std::mutex> lk(mu_);
+				spare_.push_back(std::move(pieces_.front()));
+				pieces_.pop_front();
+				cv_.notify_all();
+			}
+			cur_ = nullptr;
+			if (last) {
+				done_ = true;
+				return 0;
+			}
+		}
 		if (!cur_) {
 			std::unique_lock<std::mutex> lk(mu_);
 			cv_.wait(lk, [&] { return (!pieces_.empty() && pieces_.front()->ready) || (seq_done_ && pieces_.empty()); });
 			if (pieces_.empty()) {
 				done_ = true;
-				break;
+				return 0;
 			}
 			cur_ = pieces_.front().get();
 			rd_ = ev_ = seg_a_ = 0;
+			spent_ = false;
 		}
 		Piece &P = *cur_;
 		const size_t lim = ev_ < P.events.size() ? (size_t)P.events[ev_].off : P.n;
-		const size_t take = std::min(n - got, lim - rd_);
-		memcpy(dst + got, P.text + rd_, take);
-		rd_ += take;
-		got += take;
-		stats.out_bytes += take;
-		if (rd_ != lim) continue;
+		if (rd_ < lim) {
+			const size_t take = std::min(maxn, lim - rd_);
+			*out = P.text + rd_;
+			rd_ += take;
+			stats.out_bytes += take;
+			return (int64_t)take;
+		}
+		// a segment is complete: its CRC joins the member's
 		const size_t seg = lim - seg_a_;
 		mcrc_ = (uint32_t)crc32_combine(mcrc_, P.seg_crc[ev_], (z_off_t)seg);
 		mlen_ += seg;
@@ -1250,7 +1271,7 @@ int64_t VcGzParallel::read(uint8_t *dst, size_t n)
 			if (mcrc_ != e.crc || (uint32_t)mlen_ != e.isize) {   // gzread stops at a failed check
 				stats.crc_error = 1;
 				done_ = true;
-				break;
+				return 0;
 			}
 			++stats.members;
 			mcrc_ = 0;
@@ -1258,15 +1279,19 @@ int64_t VcGzParallel::read(uint8_t *dst, size_t n)
 			++ev_;
 			continue;
 		}
-		const bool last = P.stream_end;
-		{
-			std::lock_guard<std::mutex> lk(mu_);
-			spare_.push_back(std::move(pieces_.front()));
-			pieces_.pop_front();
-			cv_.notify_all();
-		}
-		cur_ = nullptr;
-		if (last) done_ = true;
+		spent_ = true;
+	}
+}
+
+int64_t VcGzParallel::read(uint8_t *dst, size_t n)
+{
+	size_t got = 0;
+	while (got < n) {
+		const uint8_t *p;
+		const int64_t k = span(&p, n - got);
+		if (k <= 0) break;
+		memcpy(dst + got, p, (size_t)k);
+		got += (size_t)k;
 	}
 	return (int64_t)got;
 }
@@ -1301,6 +1326,8 @@ VcGzParallel *vc_gzp_open(const char *path, int threads, uint64_t chunk_bytes)
 }
 
 int64_t vc_gzp_read(VcGzParallel *g, uint8_t *dst, size_t n) { return g->read(dst, n); }
+
+int64_t vc_gzp_span(VcGzParallel *g, const uint8_t **p, size_t max) { return g->span(p, max); }
 
 void vc_gzp_stats(VcGzParallel *g, VcGzStats *st) { g->get_stats(st); }
 

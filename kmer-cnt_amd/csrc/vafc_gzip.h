@@ -51,6 +51,9 @@ class VcGzParallel;
 VcGzParallel *vc_gzp_open(const char *path, int threads, uint64_t chunk_bytes);
 // Next bytes of the decompressed stream, in order: > 0 bytes, 0 at the end.
 int64_t vc_gzp_read(VcGzParallel *g, uint8_t *dst, size_t n);
+// The same without a copy: up to `max` next bytes at *p, valid until the next
+// call on g.
+int64_t vc_gzp_span(VcGzParallel *g, const uint8_t **p, size_t max);
 void vc_gzp_stats(VcGzParallel *g, VcGzStats *st);
 void vc_gzp_close(VcGzParallel *g);
 

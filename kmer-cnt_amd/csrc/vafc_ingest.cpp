@@ -396,7 +396,7 @@ extern "C" int vc_scan_file_parallel(const char *path, int k, int block_bases, i
                                      uint64_t piece_bytes, vc_file_stats *st, uint8_t *seq_out, size_t seq_cap,
                                      uint32_t *lens_out, size_t lens_cap)
 {
-	if (!path || !st || n_threads < 1 || piece_bytes < 2) return VC_EINVAL;
+	if (!path || !st || n_threads < 1) return VC_EINVAL;
 	vc_file_stats local = {0, 0, 0, 0.0};
 	const double t0 = mono_now();
 	const int fd = open(path, O_RDONLY);
@@ -424,6 +424,10 @@ extern "C" int vc_scan_file_parallel(const char *path, int k, int block_bases, i
 		local.seconds = mono_now() - t0;
 		*st = local;
 		return rc;
+	}
+	if (piece_bytes < 2) {
+		close(fd);
+		return VC_EINVAL;
 	}
 	HostSink sink(n_threads + 2, piece_bytes, seq_out, seq_cap, lens_out, lens_cap);
 	const int rc = vc_ingest_plain(fd, (uint64_t)sb.st_size, k, block_bases, n_threads, n_threads + 2,
