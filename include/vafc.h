@@ -42,7 +42,8 @@ enum {
 	VC_EHIP = -3,        /* HIP runtime / kernel launch error */
 	VC_ENODEV = -4,      /* no usable GPU */
 	VC_EIO = -5,         /* file could not be opened / read */
-	VC_ETOOMANY = -6     /* more than INT32_MAX>>1 patterns (vaf-counter.c:205-209) */
+	VC_ETOOMANY = -6,    /* more than INT32_MAX>>1 patterns (vaf-counter.c:205-209) */
+	VC_EFULL = -7        /* k-mer histogram: more distinct k-mers than the table holds */
 };
 
 typedef struct vc_ctx vc_ctx;
@@ -220,6 +221,33 @@ const uint8_t *vc_fasta_seq(const vc_fasta *fa, int i, uint32_t *len);
 int vc_fasta_data(const vc_fasta *fa, const uint8_t **seq, size_t *bytes, const uint64_t **offs,
                   const uint32_t **lens);
 void vc_fasta_free(vc_fasta *fa);
+
+/* ------------------------------------------------------------------ */
+/* kc-c4: histogram of canonical k-mer occurrence counts               */
+/* (kc-c4.c)                                   */
+/* ------------------------------------------------------------------ */
+
+/* A counter in histogram mode: every canonical k-mer (seq_nt4_table decode,
+ * kc-c4.c:85-101) of the reads given to vc_count_block / vc_count_device /
+ * vc_count_file is counted in a device hash table of `table_slots` slots
+ * (16 B each, rounded up to a power of two; 0 = sized from free HBM).
+ * Replaces kc-c4's kc_c4x_t sub-tables and count_file (kc-c4.c:56-66,
+ * 170-182).  vc_reset clears the table; vc_finish returns the k-mers seen. */
+int vc_kc_create(vc_ctx **out, int k, uint64_t table_slots, int device);
+/* Count only the k-mers of partition `part` of `n_parts` (by the low 32 bits
+ * h of hash64, kc-c4.c:40-50: (h * n_parts) >> 32 == part), the way kc-c4
+ * splits k-mers over 2^p sub-tables by hash (kc-c4.c:74-83): a set larger
+ * than the table is counted in n_parts passes, or on n_parts GPUs, whose
+ * histograms add up.  n_parts = 1 counts everything.  Clears the table. */
+int vc_kc_set_partition(vc_ctx *ctx, uint32_t n_parts, uint32_t part);
+/* Slots of the table (after rounding). */
+uint64_t vc_kc_slots(vc_ctx *ctx);
+/* Synchronizes; hist[c] (c = 1..255, 256 entries) += the number of distinct
+ * k-mers counted min(c, 255) times (print_hist, kc-c4.c:196-223); distinct
+ * and kmers receive the table's distinct k-mers and the k-mers seen.
+ * VC_EFULL (hist untouched) when the table ran out of room: count again
+ * with more partitions or a larger table. */
+int vc_kc_histogram(vc_ctx *ctx, uint64_t *hist, uint64_t *distinct, uint64_t *kmers);
 
 /* Decode mode of a counter: on = seq_nt4_table at every position, the decode
  * of snp-pattern-gen (snp-pattern-gen.c:165), instead of vaf-counter's

@@ -27,6 +27,7 @@
 #include "vafc_fastq.h"
 #include "vafc_ingest.h"
 #include "vafc_internal.h"
+#include "vafc_kc.h"
 
 #define HIPCK(call)                                                                         \
 	do {                                                                                    \
@@ -255,6 +256,20 @@ struct vc_ctx {
 	std::vector<Slot> islot;               // parallel ingest (vc_count_file on plain files)
 	bool timing = false, timed = false;
 	hipEvent_t t0 = nullptr, t1 = nullptr;
+	struct Kc *kc = nullptr;               // histogram mode (vc_kc_create)
+};
+
+// kc-c4 histogram mode: the device hash table and its bookkeeping
+struct Kc {
+	unsigned long long *d_table = nullptr;   // 2 * slots
+	uint64_t slots = 0;
+	uint32_t tbits = 0;
+	uint32_t n_parts = 1, part = 0;
+	unsigned long long *d_stats = nullptr;   // k-mers, distinct, overflow
+	unsigned long long *d_hist = nullptr;    // 256
+	uint32_t *d_nlong = nullptr, *d_long = nullptr;
+	uint64_t *d_segstart = nullptr;
+	uint32_t long_cap = 0;
 };
 
 static int ensure_long_cap(vc_ctx *c, uint64_t seq_bytes)
@@ -414,15 +429,68 @@ extern "C" void vc_destroy(vc_ctx *c)
 	if (c->d_nlong) (void)hipFree(c->d_nlong);
 	if (c->d_pad) (void)hipFree(c->d_pad);
 	if (c->d_long) (void)hipFree(c->d_long);
+	if (c->kc) {
+		Kc &K = *c->kc;
+		for (void *q : {(void *)K.d_table, (void *)K.d_stats, (void *)K.d_hist, (void *)K.d_nlong, (void *)K.d_long,
+		                (void *)K.d_segstart})
+			if (q) (void)hipFree(q);
+		delete c->kc;
+	}
 	if (c->st) (void)hipStreamDestroy(c->st);
 	delete c;
 }
 
 // Enqueue the two counting kernels over device-resident reads on stream st.
+static int kc_launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint64_t *d_offs,
+                     const uint32_t *d_lens, uint64_t n_reads, hipStream_t st)
+{
+	Kc &K = *c->kc;
+	const uint64_t need = seq_bytes / (KC_LONG + 1) + 1;
+	if (need > K.long_cap) {
+		HIPCK(hipStreamSynchronize(st));
+		if (K.d_long) HIPCK(hipFree(K.d_long));
+		if (K.d_segstart) HIPCK(hipFree(K.d_segstart));
+		K.d_long = nullptr;
+		K.d_segstart = nullptr;
+		const uint64_t cap = need < 0xFFFFFFF0ull ? need : 0xFFFFFFF0ull;
+		HIPCK(hipMalloc(&K.d_long, cap * sizeof(uint32_t)));
+		HIPCK(hipMalloc(&K.d_segstart, (cap + 1) * sizeof(uint64_t)));
+		K.long_cap = (uint32_t)cap;
+	}
+	KcArgs A;
+	A.seq = d_seq;
+	A.offs = d_offs;
+	A.lens = d_lens;
+	A.n_reads = n_reads;
+	A.table = K.d_table;
+	A.tmask = K.slots - 1;
+	A.tbits = K.tbits;
+	A.n_parts = K.n_parts;
+	A.part = K.part;
+	A.k = c->k;
+	A.kmask = ((uint64_t)1 << (2 * c->k)) - 1;
+	A.stats = K.d_stats;
+	A.nlong = K.d_nlong;
+	A.longlist = K.d_long;
+	A.long_cap = K.long_cap;
+	A.segstart = K.d_segstart;
+	const uint64_t blocks = (n_reads + KC_THREADS - 1) / KC_THREADS;
+	const uint64_t maxg = (uint64_t)c->n_cu * 16;
+	const int grid = (int)(blocks < maxg ? blocks : maxg);
+	if (c->timing) HIPCK(hipEventRecord(c->t0, st));
+	HIPCK(vc_launch_kc(&A, grid, st));
+	if (c->timing) {
+		HIPCK(hipEventRecord(c->t1, st));
+		c->timed = true;
+	}
+	return VC_OK;
+}
+
 static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint64_t *d_offs,
                   const uint32_t *d_lens, uint64_t n_reads, hipStream_t st)
 {
 	if (n_reads == 0) return VC_OK;
+	if (c->kc) return kc_launch(c, d_seq, seq_bytes, d_offs, d_lens, n_reads, st);
 	int rc = ensure_long_cap(c, seq_bytes);
 	if (rc != VC_OK) return rc;
 	VcKernelArgs A;
@@ -559,6 +627,14 @@ extern "C" int vc_finish(vc_ctx *c, uint32_t *counts, uint64_t *kmers)
 	HIPCK(hipStreamSynchronize(c->st));
 	HIPCK(hipDeviceSynchronize());
 	for (auto &s : c->slot) s.pending = false;
+	if (c->kc) {   // histogram mode: the k-mers seen (vc_kc_histogram gives the rest)
+		if (kmers) {
+			unsigned long long st[3];
+			HIPCK(hipMemcpy(st, c->kc->d_stats, sizeof st, hipMemcpyDeviceToHost));
+			*kmers = st[0];
+		}
+		return VC_OK;
+	}
 	if (counts)
 		HIPCK(hipMemcpy(counts, c->d_counts, 2 * (size_t)c->n_patterns * sizeof(uint32_t),
 		                hipMemcpyDeviceToHost));
@@ -574,6 +650,11 @@ extern "C" int vc_reset(vc_ctx *c)
 {
 	if (!c) return VC_EINVAL;
 	HIPCK(hipSetDevice(c->dev));
+	if (c->kc) {
+		HIPCK(hipMemsetAsync(c->kc->d_table, 0, c->kc->slots * 16, c->st));
+		HIPCK(hipMemsetAsync(c->kc->d_stats, 0, 3 * sizeof(unsigned long long), c->st));
+		return VC_OK;
+	}
 	HIPCK(hipMemsetAsync(c->d_counts, 0, 2 * (size_t)c->n_patterns * sizeof(uint32_t), c->st));
 	HIPCK(hipMemsetAsync(c->d_tally, 0, sizeof(unsigned long long), c->st));
 	return VC_OK;
@@ -907,6 +988,87 @@ extern "C" int vc_debug_decode(const uint8_t *d_seq, size_t seq_bytes, const uin
 	return VC_OK;
 }
 
+// ---------------------------------------------------------------------------
+// kc-c4 histogram mode (vafc_kc.hip)
+// ---------------------------------------------------------------------------
+
+extern "C" int vc_kc_create(vc_ctx **out, int k, uint64_t table_slots, int device)
+{
+	if (!out) return VC_EINVAL;
+	*out = nullptr;
+	vc_ctx *c = nullptr;
+	int rc = vc_create(&c, k, nullptr, nullptr, 0, 0, device);
+	if (rc != VC_OK) return rc;
+	Kc *K = new (std::nothrow) Kc;
+	if (!K) {
+		vc_destroy(c);
+		return VC_ENOMEM;
+	}
+	c->kc = K;
+	if (table_slots == 0) {   // about 60 % of free HBM
+		size_t fr = 0, tot = 0;
+		if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = (size_t)1 << 30;
+		table_slots = (uint64_t)(fr * 0.6) / 16;
+	}
+	uint32_t tbits = 10;
+	while (tbits < 40 && ((uint64_t)1 << tbits) < table_slots) ++tbits;
+	if (((uint64_t)1 << tbits) > table_slots && tbits > 10) {
+		size_t fr = 0, tot = 0;   // round down when rounding up would not fit
+		if (hipMemGetInfo(&fr, &tot) == hipSuccess && ((uint64_t)16 << tbits) > (uint64_t)fr * 0.9) --tbits;
+	}
+	K->tbits = tbits;
+	K->slots = (uint64_t)1 << tbits;
+	if (hipMalloc(&K->d_table, K->slots * 16) != hipSuccess || hipMalloc(&K->d_stats, 3 * 8) != hipSuccess ||
+	    hipMalloc(&K->d_hist, 256 * 8) != hipSuccess || hipMalloc(&K->d_nlong, 4) != hipSuccess) {
+		vc_destroy(c);
+		return VC_EHIP;
+	}
+	rc = vc_reset(c);
+	if (rc == VC_OK && hipStreamSynchronize(c->st) != hipSuccess) rc = VC_EHIP;
+	if (rc != VC_OK) {
+		vc_destroy(c);
+		return rc;
+	}
+	*out = c;
+	return VC_OK;
+}
+
+extern "C" int vc_kc_set_partition(vc_ctx *c, uint32_t n_parts, uint32_t part)
+{
+	if (!c || !c->kc || n_parts == 0 || part >= n_parts) return VC_EINVAL;
+	HIPCK(hipSetDevice(c->dev));
+	HIPCK(hipStreamSynchronize(c->st));
+	c->kc->n_parts = n_parts;
+	c->kc->part = part;
+	return vc_reset(c);
+}
+
+extern "C" uint64_t vc_kc_slots(vc_ctx *c) { return c && c->kc ? c->kc->slots : 0; }
+
+extern "C" int vc_kc_histogram(vc_ctx *c, uint64_t *hist, uint64_t *distinct, uint64_t *kmers)
+{
+	if (!c || !c->kc) return VC_EINVAL;
+	Kc &K = *c->kc;
+	HIPCK(hipSetDevice(c->dev));
+	HIPCK(hipStreamSynchronize(c->st));
+	unsigned long long st[3];
+	HIPCK(hipMemcpy(st, K.d_stats, sizeof st, hipMemcpyDeviceToHost));
+	if (distinct) *distinct = st[1];
+	if (kmers) *kmers = st[0];
+	if (st[2] || st[1] > K.slots / 100 * 85) return VC_EFULL;
+	if (hist) {
+		HIPCK(hipMemsetAsync(K.d_hist, 0, 256 * 8, c->st));
+		const uint64_t blocks = (K.slots + 255) / 256;
+		const uint64_t maxg = (uint64_t)c->n_cu * 8;
+		HIPCK(vc_launch_kc_hist(K.d_table, K.slots, K.d_hist, (int)(blocks < maxg ? blocks : maxg), c->st));
+		unsigned long long h[256];
+		HIPCK(hipMemcpyAsync(h, K.d_hist, sizeof h, hipMemcpyDeviceToHost, c->st));
+		HIPCK(hipStreamSynchronize(c->st));
+		for (int i = 0; i < 256; ++i) hist[i] += h[i];
+	}
+	return VC_OK;
+}
+
 extern "C" const char *vc_strerror(int err)
 {
 	switch (err) {
@@ -917,6 +1079,7 @@ extern "C" const char *vc_strerror(int err)
 	case VC_ENODEV: return "no HIP device";
 	case VC_EIO: return "file could not be opened";
 	case VC_ETOOMANY: return "too many patterns";
+	case VC_EFULL: return "k-mer table full";
 	default: return "unknown error";
 	}
 }

@@ -28,7 +28,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VAFC_LIB", os.path.join(_HERE, "lib", "libvafc.so"))
 
-VC_OK, VC_EINVAL, VC_ENOMEM, VC_EHIP, VC_ENODEV, VC_EIO, VC_ETOOMANY = 0, -1, -2, -3, -4, -5, -6
+VC_OK, VC_EINVAL, VC_ENOMEM, VC_EHIP, VC_ENODEV, VC_EIO, VC_ETOOMANY, VC_EFULL = 0, -1, -2, -3, -4, -5, -6, -7
 
 # every symbol include/vafc.h declares
 EXPORTS = (
@@ -40,6 +40,7 @@ EXPORTS = (
     "vc_gz_inflate_parallel", "vc_gz_inflate_zlib", "vc_gz_crc32",
     "vc_fasta_load", "vc_fasta_count", "vc_fasta_name", "vc_fasta_seq", "vc_fasta_data", "vc_fasta_free",
     "vc_count_candidates", "vc_set_nt4_decode",
+    "vc_kc_create", "vc_kc_set_partition", "vc_kc_slots", "vc_kc_histogram",
     "vc_synth_reads",
     "vc_debug_decode", "vc_strerror", "vc_version",
 )
@@ -123,6 +124,10 @@ def lib():
         "vc_set_nt4_decode": (C.c_int, [P, C.c_int]),
         "vc_count_candidates": (C.c_int, [C.c_int, P, C.c_size_t, P, P, C.c_uint64, P, C.c_size_t, P,
                                           C.c_int]),
+        "vc_kc_create": (C.c_int, [C.POINTER(P), C.c_int, C.c_uint64, C.c_int]),
+        "vc_kc_set_partition": (C.c_int, [P, C.c_uint32, C.c_uint32]),
+        "vc_kc_slots": (C.c_uint64, [P]),
+        "vc_kc_histogram": (C.c_int, [P, P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "vc_synth_reads": (C.c_int, [P, P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
                                      C.c_double, P, P, C.c_uint32, P]),
         "vc_debug_decode": (C.c_int, [P, C.c_size_t, P, P, C.c_uint64, P, P]),
@@ -574,3 +579,100 @@ def count_candidate_kmers(k: int, seqs, keys, device: int = 0) -> np.ndarray:
                                   len(seqs), _ptr(keys), keys.size, _ptr(counts), device),
         "vc_count_candidates")
     return counts[:keys.size]
+
+
+# --------------------------------------------------------------------------
+# kc-c4 k-mer histogram
+# --------------------------------------------------------------------------
+
+class KmerHistogram(KmerMap):
+    """kc-c4's kc_c4x_t (kc-c4.c:52-67) on the GPU: every canonical k-mer of the
+    reads counted in one device hash table of ``slots`` 16-byte slots (0 = sized
+    from free HBM).  count_block / count_device / count_file as for KmerMap;
+    ``histogram()`` is print_hist's count vector (kc-c4.c:219-231)."""
+
+    def __init__(self, k: int, slots: int = 0, device: int = 0):
+        self.k, self.n_patterns, self.device = k, 0, device
+        h = P()
+        _ck(lib().vc_kc_create(C.byref(h), k, slots, device), "vc_kc_create")
+        self._h = h
+        self.n_collisions = 0
+
+    @property
+    def slots(self) -> int:
+        return lib().vc_kc_slots(self._h)
+
+    def set_partition(self, n_parts: int, part: int) -> None:
+        """Count only hash slice ``part`` of ``n_parts`` (clears the table)."""
+        _ck(lib().vc_kc_set_partition(self._h, n_parts, part), "vc_kc_set_partition")
+
+    def histogram(self):
+        """(hist uint64[256], distinct, kmers): hist[c] = distinct k-mers seen
+        min(c, 255) times.  Raises VafcError(VC_EFULL) when the table ran out."""
+        hist = np.zeros(256, np.uint64)
+        d, km = C.c_uint64(), C.c_uint64()
+        _ck(lib().vc_kc_histogram(self._h, _ptr(hist), C.byref(d), C.byref(km)), "vc_kc_histogram")
+        return hist, d.value, km.value
+
+
+def kc_count_file(fn: str, k: int = 31, block_size: int = 10_000_000, n_thread: int = 4,
+                  slots: int = 0, device: int = 0) -> np.ndarray:
+    """count_file + print_hist's counts (kc-c4.c:181-231): hist uint64[256].
+    A table too small for the distinct k-mers is re-run in hash slices."""
+    h = KmerHistogram(k, slots, device)
+    try:
+        n_parts = 1
+        while True:
+            total = np.zeros(256, np.uint64)
+            kmers, full = 0, False
+            for part in range(n_parts):
+                h.set_partition(n_parts, part)
+                h.count_file(fn, block_size, n_thread)
+                h.finish()
+                try:
+                    hist, _, kmers = h.histogram()
+                except VafcError as e:
+                    if e.code != VC_EFULL:
+                        raise
+                    full = True
+                    break
+                total += hist
+            if not full:
+                return total
+            cap = h.slots * 7 // 10
+            n_parts = max(n_parts * 2, -(-kmers // cap) if cap else 2)
+    finally:
+        h.close()
+
+
+def kc_main(argv=None) -> int:
+    """kc-c4's main (kc-c4.c:236-265): prints ``i\tcount`` for i = 1..255."""
+    import getopt
+    argv = sys.argv[1:] if argv is None else argv
+    k, p, b, t = 31, 10, 10_000_000, 4
+    try:
+        opts, args = getopt.gnu_getopt(argv, "k:p:b:t:")
+    except getopt.GetoptError:
+        opts, args = [], []
+    for o, v in opts:
+        if o == "-k":
+            k = int(v)
+        elif o == "-p":
+            p = int(v)
+        elif o == "-b":
+            b = int(v)
+        elif o == "-t":
+            t = int(v)
+    if not args:
+        sys.stderr.write("Usage: kc-c4 [options] <in.fa>\nOptions:\n"
+                         "  -k INT     k-mer size [%d]\n  -p INT     prefix length [%d]\n"
+                         "  -b INT     block size [%d]\n  -t INT     number of worker threads [%d]\n"
+                         % (k, p, b, t))
+        return 1
+    if p < 10:
+        sys.stderr.write("ERROR: -p should be at least 10\n")
+        return 1
+    hist = kc_count_file(args[0], k, b, t, int(os.environ.get("VAFC_KC_SLOTS", "0")),
+                         int(os.environ.get("VAFC_DEVICE", "0")))
+    sys.stdout.write("".join("%d\t%d\n" % (i, hist[i]) for i in range(1, 256)))
+    return 0
