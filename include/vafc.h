@@ -230,15 +230,17 @@ void vc_fasta_free(vc_fasta *fa);
 /* A counter in histogram mode: every canonical k-mer (seq_nt4_table decode,
  * kc-c4.c:85-101) of the reads given to vc_count_block / vc_count_device /
  * vc_count_file is counted in a device hash table of `table_slots` slots
- * (16 B each, rounded up to a power of two; 0 = sized from free HBM).
+ * (16 B each, rounded up to a power of two, at most 40 % of free HBM; 0 =
+ * that maximum).
  * Replaces kc-c4's kc_c4x_t sub-tables and count_file (kc-c4.c:56-66,
  * 170-182).  vc_reset clears the table; vc_finish returns the k-mers seen. */
 int vc_kc_create(vc_ctx **out, int k, uint64_t table_slots, int device);
-/* Count only the k-mers of partition `part` of `n_parts` (by the low 32 bits
- * h of hash64, kc-c4.c:40-50: (h * n_parts) >> 32 == part), the way kc-c4
- * splits k-mers over 2^p sub-tables by hash (kc-c4.c:74-83): a set larger
- * than the table is counted in n_parts passes, or on n_parts GPUs, whose
- * histograms add up.  n_parts = 1 counts everything.  Clears the table. */
+/* Count only the k-mers of partition `part` of `n_parts` (1..1024), by the
+ * low 10 bits of hash64 (kc-c4.c:40-50): ((h & 1023) * n_parts) >> 10 ==
+ * part, so a partition holds whole kc-c4 / yak sub-tables (kc-c4.c:74-83,
+ * p >= 10): a set larger than the table is counted in n_parts passes, or on
+ * n_parts GPUs, whose histograms add up.  n_parts = 1 counts everything.
+ * Clears the table. */
 int vc_kc_set_partition(vc_ctx *ctx, uint32_t n_parts, uint32_t part);
 /* Slots of the table (after rounding). */
 uint64_t vc_kc_slots(vc_ctx *ctx);
@@ -248,6 +250,25 @@ uint64_t vc_kc_slots(vc_ctx *ctx);
  * VC_EFULL (hist untouched) when the table ran out of room: count again
  * with more partitions or a larger table. */
 int vc_kc_histogram(vc_ctx *ctx, uint64_t *hist, uint64_t *distinct, uint64_t *kmers);
+/* General form: hist[min(c, n_bins - 1)] += 1 (n_bins 2..1024) for every key
+ * counted c >= min_count times and not dropped by vc_yak_bloom_select;
+ * *distinct = the keys added.  yak-count's histogram (yak-count.c:209-240,
+ * 500-503) is n_bins 1024, min_count 1 (no filter) or 2 (after its shrink to
+ * [2, 1023], :268-288). */
+int vc_kc_histogram2(vc_ctx *ctx, uint64_t *hist, uint32_t n_bins, uint64_t min_count, uint64_t *distinct,
+                     uint64_t *kmers);
+
+/* yak-count -b (yak-count.c:440-452), pass 1 to pass 2.  Count file 1 with
+ * first-occurrence tracking on (vc_kc_track_first, which also clears), then
+ * vc_yak_bloom_select replays yak's per-sub-table blocked Bloom filters
+ * (2^(bf_shift - pre) bits each, n_hash bits per k-mer, yak-count.c:71-108,
+ * 150-176) over the stream order to find the keys yak would have inserted,
+ * restarts their counts at 0 and drops the rest; later count calls (file 2)
+ * then only count those keys (yak's create_new = 0).  Without a valid filter
+ * (n_hash <= 0, or bf_shift - pre outside 9..55) every key stays.  A later
+ * vc_reset returns to insert mode. */
+int vc_kc_track_first(vc_ctx *ctx, int on);
+int vc_yak_bloom_select(vc_ctx *ctx, int pre, int bf_shift, int n_hash);
 
 /* Decode mode of a counter: on = seq_nt4_table at every position, the decode
  * of snp-pattern-gen (snp-pattern-gen.c:165), instead of vaf-counter's

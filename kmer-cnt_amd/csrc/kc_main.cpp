@@ -8,7 +8,8 @@
 // sub-table count) does not change the output and only has its check kept.
 // When the distinct k-mers outgrow the table ($VAFC_KC_SLOTS, default sized
 // from free HBM) the file is counted again in hash partitions whose
-// histograms add up (vc_kc_set_partition).
+// histograms add up (vc_kc_set_partition).  The table is sized from the input
+// file (at most 40 % of free HBM).
 //
 // Differences, all on failure paths: an input that cannot be opened prints
 // an error and exits 1 (the reference dereferences a null table,
@@ -16,8 +17,22 @@
 #include <getopt.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
 
 #include "vafc.h"
+
+// Table size from the input: at most one distinct k-mer per byte of the file
+// (five per byte of gzip), so no partition pass is needed unless HBM caps it.
+static uint64_t size_hint(const char *fn)
+{
+	struct stat sb;
+	if (stat(fn, &sb) != 0 || sb.st_size <= 0) return 1 << 16;
+	uint64_t b = (uint64_t)sb.st_size;
+	const size_t n = strlen(fn);
+	if (n > 3 && strcmp(fn + n - 3, ".gz") == 0) b *= 5;
+	return b + b / 4 + (1 << 16);
+}
 
 int main(int argc, char *argv[])
 {
@@ -50,8 +65,8 @@ int main(int argc, char *argv[])
 	const char *dev_env = getenv("VAFC_DEVICE");
 	const int device = dev_env ? atoi(dev_env) : 0;
 	const char *slots_env = getenv("VAFC_KC_SLOTS");
-	const uint64_t slots = slots_env ? strtoull(slots_env, nullptr, 10) : 0;
 	const char *fn = argv[optind];
+	const uint64_t slots = slots_env ? strtoull(slots_env, nullptr, 10) : size_hint(fn);
 
 	vc_ctx *ctx = nullptr;
 	int rc = vc_kc_create(&ctx, k, slots, device);
@@ -94,7 +109,7 @@ int main(int argc, char *argv[])
 		const uint64_t cap = vc_kc_slots(ctx) / 10 * 7;
 		uint64_t want = cap ? (kmers + cap - 1) / cap : 2;
 		if (want <= n_parts) want = (uint64_t)n_parts * 2;
-		if (want > 65536) {
+		if (want > 1024) {
 			fprintf(stderr, "ERROR: k-mer table too small\n");
 			vc_destroy(ctx);
 			return 1;

@@ -266,10 +266,13 @@ struct Kc {
 	uint32_t tbits = 0;
 	uint32_t n_parts = 1, part = 0;
 	unsigned long long *d_stats = nullptr;   // k-mers, distinct, overflow
-	unsigned long long *d_hist = nullptr;    // 256
+	unsigned long long *d_hist = nullptr;    // up to 1024 bins + the slots counted
 	uint32_t *d_nlong = nullptr, *d_long = nullptr;
 	uint64_t *d_segstart = nullptr;
 	uint32_t long_cap = 0;
+	uint64_t *d_first = nullptr;             // first-occurrence stamps (vc_kc_track_first)
+	bool track_first = false, lookup_only = false;
+	uint64_t read_base = 0;                  // reads launched since the last reset
 };
 
 static int ensure_long_cap(vc_ctx *c, uint64_t seq_bytes)
@@ -432,7 +435,7 @@ extern "C" void vc_destroy(vc_ctx *c)
 	if (c->kc) {
 		Kc &K = *c->kc;
 		for (void *q : {(void *)K.d_table, (void *)K.d_stats, (void *)K.d_hist, (void *)K.d_nlong, (void *)K.d_long,
-		                (void *)K.d_segstart})
+		                (void *)K.d_segstart, (void *)K.d_first})
 			if (q) (void)hipFree(q);
 		delete c->kc;
 	}
@@ -467,6 +470,10 @@ static int kc_launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const ui
 	A.tbits = K.tbits;
 	A.n_parts = K.n_parts;
 	A.part = K.part;
+	A.first = K.track_first && !K.lookup_only ? K.d_first : nullptr;
+	A.read_base = K.read_base;
+	A.lookup_only = K.lookup_only ? 1 : 0;
+	K.read_base += n_reads;
 	A.k = c->k;
 	A.kmask = ((uint64_t)1 << (2 * c->k)) - 1;
 	A.stats = K.d_stats;
@@ -651,8 +658,12 @@ extern "C" int vc_reset(vc_ctx *c)
 	if (!c) return VC_EINVAL;
 	HIPCK(hipSetDevice(c->dev));
 	if (c->kc) {
-		HIPCK(hipMemsetAsync(c->kc->d_table, 0, c->kc->slots * 16, c->st));
-		HIPCK(hipMemsetAsync(c->kc->d_stats, 0, 3 * sizeof(unsigned long long), c->st));
+		Kc &K = *c->kc;
+		HIPCK(hipMemsetAsync(K.d_table, 0, K.slots * 16, c->st));
+		HIPCK(hipMemsetAsync(K.d_stats, 0, 3 * sizeof(unsigned long long), c->st));
+		if (K.track_first) HIPCK(hipMemsetAsync(K.d_first, 0xFF, K.slots * 8, c->st));
+		K.read_base = 0;
+		K.lookup_only = false;
 		return VC_OK;
 	}
 	HIPCK(hipMemsetAsync(c->d_counts, 0, 2 * (size_t)c->n_patterns * sizeof(uint32_t), c->st));
@@ -1005,21 +1016,21 @@ extern "C" int vc_kc_create(vc_ctx **out, int k, uint64_t table_slots, int devic
 		return VC_ENOMEM;
 	}
 	c->kc = K;
-	if (table_slots == 0) {   // about 60 % of free HBM
-		size_t fr = 0, tot = 0;
-		if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = (size_t)1 << 30;
-		table_slots = (uint64_t)(fr * 0.6) / 16;
-	}
-	uint32_t tbits = 10;
-	while (tbits < 40 && ((uint64_t)1 << tbits) < table_slots) ++tbits;
-	if (((uint64_t)1 << tbits) > table_slots && tbits > 10) {
-		size_t fr = 0, tot = 0;   // round down when rounding up would not fit
-		if (hipMemGetInfo(&fr, &tot) == hipSuccess && ((uint64_t)16 << tbits) > (uint64_t)fr * 0.9) --tbits;
+	// at most 40 % of free HBM (rounded down to a power of two), so first-
+	// occurrence stamps and yak's scratch table still fit beside it
+	size_t fr = 0, tot = 0;
+	if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = (size_t)1 << 30;
+	uint32_t cap_bits = 10;
+	while (cap_bits < 40 && ((uint64_t)32 << cap_bits) <= (uint64_t)(fr * 0.4)) ++cap_bits;
+	uint32_t tbits = cap_bits;
+	if (table_slots) {
+		tbits = 10;
+		while (tbits < cap_bits && ((uint64_t)1 << tbits) < table_slots) ++tbits;
 	}
 	K->tbits = tbits;
 	K->slots = (uint64_t)1 << tbits;
 	if (hipMalloc(&K->d_table, K->slots * 16) != hipSuccess || hipMalloc(&K->d_stats, 3 * 8) != hipSuccess ||
-	    hipMalloc(&K->d_hist, 256 * 8) != hipSuccess || hipMalloc(&K->d_nlong, 4) != hipSuccess) {
+	    hipMalloc(&K->d_hist, 1025 * 8) != hipSuccess || hipMalloc(&K->d_nlong, 4) != hipSuccess) {
 		vc_destroy(c);
 		return VC_EHIP;
 	}
@@ -1035,7 +1046,7 @@ extern "C" int vc_kc_create(vc_ctx **out, int k, uint64_t table_slots, int devic
 
 extern "C" int vc_kc_set_partition(vc_ctx *c, uint32_t n_parts, uint32_t part)
 {
-	if (!c || !c->kc || n_parts == 0 || part >= n_parts) return VC_EINVAL;
+	if (!c || !c->kc || n_parts == 0 || n_parts > 1024 || part >= n_parts) return VC_EINVAL;
 	HIPCK(hipSetDevice(c->dev));
 	HIPCK(hipStreamSynchronize(c->st));
 	c->kc->n_parts = n_parts;
@@ -1045,27 +1056,111 @@ extern "C" int vc_kc_set_partition(vc_ctx *c, uint32_t n_parts, uint32_t part)
 
 extern "C" uint64_t vc_kc_slots(vc_ctx *c) { return c && c->kc ? c->kc->slots : 0; }
 
-extern "C" int vc_kc_histogram(vc_ctx *c, uint64_t *hist, uint64_t *distinct, uint64_t *kmers)
+// hist[0..n_bins) on the host += the device histogram; *counted = slots in it
+static int kc_hist(vc_ctx *c, uint64_t *hist, uint32_t n_bins, uint64_t min_count, uint64_t *counted)
 {
-	if (!c || !c->kc) return VC_EINVAL;
+	Kc &K = *c->kc;
+	HIPCK(hipMemsetAsync(K.d_hist, 0, 1025 * 8, c->st));
+	const uint64_t blocks = (K.slots + 255) / 256;
+	const uint64_t maxg = (uint64_t)c->n_cu * 8;
+	HIPCK(vc_launch_kc_hist(K.d_table, K.slots, K.d_hist, n_bins, min_count, (int)(blocks < maxg ? blocks : maxg),
+	                        c->st));
+	std::vector<unsigned long long> h(n_bins + 1);
+	HIPCK(hipMemcpyAsync(h.data(), K.d_hist, (n_bins + 1) * 8, hipMemcpyDeviceToHost, c->st));
+	HIPCK(hipStreamSynchronize(c->st));
+	if (hist)
+		for (uint32_t i = 0; i < n_bins; ++i) hist[i] += h[i];
+	if (counted) *counted = h[n_bins];
+	return VC_OK;
+}
+
+extern "C" int vc_kc_histogram2(vc_ctx *c, uint64_t *hist, uint32_t n_bins, uint64_t min_count, uint64_t *distinct,
+                                uint64_t *kmers)
+{
+	if (!c || !c->kc || n_bins < 2 || n_bins > 1024) return VC_EINVAL;
 	Kc &K = *c->kc;
 	HIPCK(hipSetDevice(c->dev));
 	HIPCK(hipStreamSynchronize(c->st));
 	unsigned long long st[3];
 	HIPCK(hipMemcpy(st, K.d_stats, sizeof st, hipMemcpyDeviceToHost));
-	if (distinct) *distinct = st[1];
 	if (kmers) *kmers = st[0];
+	if (distinct) *distinct = st[1];
 	if (st[2] || st[1] > K.slots / 100 * 85) return VC_EFULL;
-	if (hist) {
-		HIPCK(hipMemsetAsync(K.d_hist, 0, 256 * 8, c->st));
-		const uint64_t blocks = (K.slots + 255) / 256;
-		const uint64_t maxg = (uint64_t)c->n_cu * 8;
-		HIPCK(vc_launch_kc_hist(K.d_table, K.slots, K.d_hist, (int)(blocks < maxg ? blocks : maxg), c->st));
-		unsigned long long h[256];
-		HIPCK(hipMemcpyAsync(h, K.d_hist, sizeof h, hipMemcpyDeviceToHost, c->st));
-		HIPCK(hipStreamSynchronize(c->st));
-		for (int i = 0; i < 256; ++i) hist[i] += h[i];
+	uint64_t counted = 0;
+	int rc = kc_hist(c, hist, n_bins, min_count, &counted);
+	if (rc == VC_OK && distinct) *distinct = counted;
+	return rc;
+}
+
+extern "C" int vc_kc_histogram(vc_ctx *c, uint64_t *hist, uint64_t *distinct, uint64_t *kmers)
+{
+	return vc_kc_histogram2(c, hist, 256, 1, distinct, kmers);
+}
+
+extern "C" int vc_kc_track_first(vc_ctx *c, int on)
+{
+	if (!c || !c->kc) return VC_EINVAL;
+	Kc &K = *c->kc;
+	HIPCK(hipSetDevice(c->dev));
+	HIPCK(hipStreamSynchronize(c->st));
+	if (on && !K.d_first && hipMalloc(&K.d_first, K.slots * 8) != hipSuccess) {
+		K.d_first = nullptr;
+		return VC_ENOMEM;
 	}
+	K.track_first = on != 0;
+	return vc_reset(c);
+}
+
+extern "C" int vc_yak_bloom_select(vc_ctx *c, int pre, int bf_shift, int n_hash)
+{
+	if (!c || !c->kc || pre < 0 || pre > 40) return VC_EINVAL;
+	Kc &K = *c->kc;
+	HIPCK(hipSetDevice(c->dev));
+	HIPCK(hipStreamSynchronize(c->st));
+	unsigned long long st[3];
+	HIPCK(hipMemcpy(st, K.d_stats, sizeof st, hipMemcpyDeviceToHost));
+	if (st[2] || st[1] > K.slots / 100 * 85) return VC_EFULL;
+	// yak_ch_init / yak_bf_init (yak-count.c:71-80, 115-121): filters exist only
+	// for n_hash > 0 and 9 <= bf_shift - pre <= 55
+	const int ns = bf_shift - pre;
+	const bool bf_on = n_hash > 0 && bf_shift > pre && ns >= 9 && ns + 9 <= 64;
+	if (bf_on && !K.track_first) return VC_EINVAL;
+	YakBloom B;
+	B.table = K.d_table;
+	B.counts_out = K.d_table;
+	B.first = K.d_first;
+	B.slots = K.slots;
+	B.pre = (uint32_t)pre;
+	B.ns = bf_on ? (uint32_t)ns : 9;
+	B.n_hash = bf_on ? (uint32_t)n_hash : 0;
+	B.wtab = nullptr;
+	B.wslots = 1;
+	B.wbits = 0;
+	B.overflow = K.d_stats + 2;
+	if (bf_on) {
+		uint64_t singles = 0;
+		std::vector<uint64_t> h(2, 0);
+		int rc = kc_hist(c, h.data(), 2, 1, nullptr);   // h[1]: keys seen exactly once
+		if (rc != VC_OK) return rc;
+		singles = h[1];
+		uint32_t wbits = 10;
+		while (wbits < 48 && ((uint64_t)1 << wbits) < 2 * singles * (uint64_t)n_hash) ++wbits;
+		B.wbits = wbits;
+		B.wslots = (uint64_t)1 << wbits;
+		// no room for the scratch table: report full, so the caller counts
+		// again in more partitions (fewer singletons per pass)
+		if (hipMalloc(&B.wtab, B.wslots * 16) != hipSuccess) return VC_EFULL;
+		HIPCK(hipMemsetAsync(B.wtab, 0, B.wslots * 16, c->st));
+	}
+	const uint64_t blocks = (K.slots + 255) / 256;
+	const uint64_t maxg = (uint64_t)c->n_cu * 8;
+	hipError_t e = vc_launch_yak_select(&B, (int)(blocks < maxg ? blocks : maxg), c->st);
+	if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+	if (B.wtab) (void)hipFree(B.wtab);
+	if (e != hipSuccess) return VC_EHIP;
+	HIPCK(hipMemcpy(st, K.d_stats, sizeof st, hipMemcpyDeviceToHost));
+	if (st[2]) return VC_EFULL;
+	K.lookup_only = true;
 	return VC_OK;
 }
 

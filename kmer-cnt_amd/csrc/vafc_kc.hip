@@ -59,29 +59,43 @@ struct Local {
 	bool overflow = false;
 };
 
-__device__ __forceinline__ void kc_insert(const KcArgs &A, uint64_t y, Local &L)
+__device__ __forceinline__ void kc_insert(const KcArgs &A, uint64_t y, uint64_t stamp, Local &L)
 {
 	const uint64_t h = kc_hash64(y, A.kmask);
-	if (A.n_parts > 1 && (uint32_t)(((h & 0xFFFFFFFFull) * A.n_parts) >> 32) != A.part) return;
+	// partitions follow the low 10 bits: whole kc-c4 / yak sub-tables (p >= 10)
+	if (A.n_parts > 1 && (uint32_t)(((h & 1023) * A.n_parts) >> 10) != A.part) return;
 	const unsigned long long key = h + 1;
 	uint64_t i = (h * 0x9E3779B97F4A7C15ull) >> (64 - A.tbits);
 	unsigned long long *T = A.table;
 	for (uint32_t probe = 0; probe < KC_MAX_PROBE; ++probe) {
 		unsigned long long cur = __hip_atomic_load(&T[2 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (A.lookup_only) {   // yak pass 2 (yak-count.c:171-175): existing keys only
+			if (cur == 0) return;
+			if (cur == key) {
+				if (__hip_atomic_load(&T[2 * i + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != KC_DROPPED)
+					atomicAdd(&T[2 * i + 1], 1ull);
+				return;
+			}
+			i = (i + 1) & A.tmask;
+			continue;
+		}
 		if (cur == 0) {
 			cur = atomicCAS(&T[2 * i], 0ull, key);
 			if (cur == 0) {
 				++L.fresh;
 				atomicAdd(&T[2 * i + 1], 1ull);
+				if (A.first) atomicMin(&A.first[i], stamp);
 				return;
 			}
 		}
 		if (cur == key) {
 			atomicAdd(&T[2 * i + 1], 1ull);
+			if (A.first) atomicMin(&A.first[i], stamp);
 			return;
 		}
 		i = (i + 1) & A.tmask;
 	}
+	if (A.lookup_only) return;
 	L.overflow = true;
 	__hip_atomic_store(&A.stats[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -89,7 +103,7 @@ __device__ __forceinline__ void kc_insert(const KcArgs &A, uint64_t y, Local &L)
 // Every canonical k-mer of bases [a, b) of a read whose windows end at or
 // after `emit_from` (kc-c4.c:85-101: an invalid base restarts the k-mer)
 __device__ __forceinline__ void kc_scan(const KcArgs &A, const uint8_t *s, uint32_t a, uint32_t b, uint32_t emit_from,
-                                        Local &L)
+                                        uint64_t read, Local &L)
 {
 	const int k = A.k;
 	const uint32_t shift = 2 * (k - 1);
@@ -102,7 +116,7 @@ __device__ __forceinline__ void kc_scan(const KcArgs &A, const uint8_t *s, uint3
 			x1 = x1 >> 2 | (uint64_t)(3 - c) << shift;
 			if (++l >= k && j >= emit_from) {
 				++L.kmers;
-				if (!L.overflow) kc_insert(A, x0 < x1 ? x0 : x1, L);
+				if (!L.overflow) kc_insert(A, x0 < x1 ? x0 : x1, (A.read_base + read) << 32 | j, L);
 			}
 		} else {
 			l = 0;
@@ -144,7 +158,7 @@ __global__ __launch_bounds__(KC_THREADS) void kc_count_kernel(KcArgs A)
 		}
 		if (!L.overflow && __hip_atomic_load(&A.stats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
 			L.overflow = true;   // the table is full: only the k-mers are tallied from here on
-		kc_scan(A, A.seq + A.offs[r], 0, len, 0, L);
+		kc_scan(A, A.seq + A.offs[r], 0, len, 0, r, L);
 	}
 	kc_flush(A, L);
 }
@@ -184,25 +198,159 @@ __global__ __launch_bounds__(KC_THREADS) void kc_long_kernel(KcArgs A)
 		const uint32_t from = s0 >= (uint32_t)(A.k - 1) ? s0 - (uint32_t)(A.k - 1) : 0;
 		if (!L.overflow && __hip_atomic_load(&A.stats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
 			L.overflow = true;
-		kc_scan(A, A.seq + A.offs[r], from, s1, s0, L);
+		kc_scan(A, A.seq + A.offs[r], from, s1, s0, r, L);
 	}
 	kc_flush(A, L);
 }
 
-// min(count, 255) of every occupied slot (kc-c4.c:196-223)
+// hist[min(count, n_bins - 1)] over the occupied slots with count >= min_count
+// (kc-c4.c:206-223: 256 bins; yak-count.c:209-240 + the shrink to [2, 1023]
+// of :268-288: 1024 bins); dropped keys are skipped.  hist[n_bins] gets the
+// number of slots counted.
 __global__ __launch_bounds__(256) void kc_hist_kernel(const unsigned long long *table, uint64_t slots,
-                                                      unsigned long long *hist)
+                                                      unsigned long long *hist, uint32_t n_bins, uint64_t min_count)
 {
-	__shared__ uint32_t h[256];
-	h[threadIdx.x] = 0;
+	__shared__ uint32_t h[1024];
+	__shared__ uint32_t tot;
+	for (uint32_t b = threadIdx.x; b < n_bins; b += blockDim.x) h[b] = 0;
+	if (threadIdx.x == 0) tot = 0;
 	__syncthreads();
+	uint32_t mine = 0;
 	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * blockDim.x) {
 		if (table[2 * i] == 0) continue;
 		const unsigned long long c = table[2 * i + 1];
-		atomicAdd(&h[c < 255 ? c : 255], 1u);
+		if (c == KC_DROPPED || c < min_count) continue;
+		atomicAdd(&h[c < n_bins - 1 ? c : n_bins - 1], 1u);
+		++mine;
 	}
+	if (mine) atomicAdd(&tot, mine);
 	__syncthreads();
-	if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+	for (uint32_t b = threadIdx.x; b < n_bins; b += blockDim.x)
+		if (h[b]) atomicAdd(&hist[b], (unsigned long long)h[b]);
+	if (threadIdx.x == 0 && tot) atomicAdd(&hist[n_bins], (unsigned long long)tot);
+}
+
+// ---- yak-count's Bloom filter, replayed (yak-count.c:91-108, 150-176) ----
+//
+// Pass 1 of yak-count -b puts a k-mer into its sub-table only when all n_hash
+// bits of its hash in that sub-table's blocked Bloom filter were set before
+// (by earlier k-mers of the stream; every k-mer sets its bits).  A k-mer seen
+// twice is therefore always kept; one seen once is kept iff each of its bits
+// was set by a k-mer occurring earlier, i.e. iff for each bit the smallest
+// first-occurrence stamp among the k-mers using that bit is below its own.
+// Only the bits of singletons matter, so they go into a scratch hash table
+// (wtab) whose values are those minimum stamps.
+
+// the n_hash bit ids of hash h: sub-table s = h & (2^pre - 1), x = h >> pre,
+// block x & (2^(ns-9) - 1), bits h1 + i*h2 mod 512 (h2 bumped off multiples
+// of 32); id = s << ns | block << 9 | bit
+struct YakBits {
+	uint64_t base;
+	uint32_t z, h2;
+};
+__device__ __forceinline__ YakBits yak_bits(uint64_t h, uint32_t pre, uint32_t ns)
+{
+	const uint64_t s = h & (((uint64_t)1 << pre) - 1), x = h >> pre;
+	const uint32_t xs = ns - 9;
+	YakBits b;
+	b.base = s << ns | (x & (((uint64_t)1 << xs) - 1)) << 9;
+	b.z = (uint32_t)(x >> xs) & 511;
+	b.h2 = (uint32_t)(x >> ns) & 511;
+	if ((b.h2 & 31) == 0) b.h2 = (b.h2 + 1) & 511;
+	return b;
+}
+
+__device__ __forceinline__ uint64_t yak_wslot(uint64_t id, uint32_t wbits)
+{
+	return (id * 0xD6E8FEB86659FD93ull) >> (64 - wbits);
+}
+
+// 1: the bit ids of every singleton into wtab (value: +inf)
+__global__ __launch_bounds__(256) void yak_wanted_kernel(YakBloom B)
+{
+	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.slots; i += (uint64_t)gridDim.x * blockDim.x) {
+		const unsigned long long key = B.table[2 * i];
+		if (key == 0 || B.table[2 * i + 1] != 1) continue;
+		YakBits b = yak_bits(key - 1, B.pre, B.ns);
+		uint32_t z = b.z;
+		for (uint32_t n = 0; n < B.n_hash; ++n, z = (z + b.h2) & 511) {
+			const unsigned long long id = (b.base | z) + 1;
+			uint64_t w = yak_wslot(id, B.wbits);
+			for (uint64_t probe = 0;; ++probe) {
+				if (probe == B.wslots) {
+					atomicOr(B.overflow, 1ull);
+					return;
+				}
+				const unsigned long long cur = atomicCAS(&B.wtab[2 * w], 0ull, id);
+				if (cur == 0) {   // new bit: no stamp yet (+inf)
+					B.wtab[2 * w + 1] = KC_DROPPED;
+					break;
+				}
+				if (cur == id) break;
+				w = (w + 1) & (B.wslots - 1);
+			}
+		}
+	}
+}
+
+// 2: for every key and each of its bits present in wtab: min(first stamp)
+__global__ __launch_bounds__(256) void yak_mintime_kernel(YakBloom B)
+{
+	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.slots; i += (uint64_t)gridDim.x * blockDim.x) {
+		const unsigned long long key = B.table[2 * i];
+		if (key == 0) continue;
+		const unsigned long long t = B.first[i];
+		YakBits b = yak_bits(key - 1, B.pre, B.ns);
+		uint32_t z = b.z;
+		for (uint32_t n = 0; n < B.n_hash; ++n, z = (z + b.h2) & 511) {
+			const unsigned long long id = (b.base | z) + 1;
+			uint64_t w = yak_wslot(id, B.wbits);
+			for (uint64_t probe = 0; probe < B.wslots; ++probe) {
+				const unsigned long long cur = B.wtab[2 * w];
+				if (cur == 0) break;
+				if (cur == id) {
+					atomicMin(&B.wtab[2 * w + 1], t);
+					break;
+				}
+				w = (w + 1) & (B.wslots - 1);
+			}
+		}
+	}
+}
+
+// 3: keep = seen twice, or a singleton whose bits were all set before it;
+// kept keys restart at count 0 (yak_ch_clear, yak-count.c:191-207), the rest
+// are dropped
+__global__ __launch_bounds__(256) void yak_select_kernel(YakBloom B)
+{
+	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.slots; i += (uint64_t)gridDim.x * blockDim.x) {
+		const unsigned long long key = B.table[2 * i];
+		if (key == 0) continue;
+		const unsigned long long c = B.table[2 * i + 1];
+		bool keep = c >= 2 || B.n_hash == 0;   // n_hash 0: no filter, every key stays
+		if (!keep && c == 1) {
+			const unsigned long long t = B.first[i];
+			YakBits b = yak_bits(key - 1, B.pre, B.ns);
+			uint32_t z = b.z;
+			keep = true;
+			for (uint32_t n = 0; n < B.n_hash && keep; ++n, z = (z + b.h2) & 511) {
+				const unsigned long long id = (b.base | z) + 1;
+				uint64_t w = yak_wslot(id, B.wbits);
+				unsigned long long m = KC_DROPPED;
+				for (uint64_t probe = 0; probe < B.wslots; ++probe) {
+					const unsigned long long cur = B.wtab[2 * w];
+					if (cur == 0) break;
+					if (cur == id) {
+						m = B.wtab[2 * w + 1];
+						break;
+					}
+					w = (w + 1) & (B.wslots - 1);
+				}
+				keep = m < t;
+			}
+		}
+		B.counts_out[2 * i + 1] = keep ? 0ull : KC_DROPPED;
+	}
 }
 
 } // namespace
@@ -218,8 +366,17 @@ extern "C" hipError_t vc_launch_kc(const KcArgs *A, int grid, hipStream_t st)
 }
 
 extern "C" hipError_t vc_launch_kc_hist(const unsigned long long *table, uint64_t slots, unsigned long long *hist,
-                                        int grid, hipStream_t st)
+                                        uint32_t n_bins, uint64_t min_count, int grid, hipStream_t st)
 {
-	hipLaunchKernelGGL(kc_hist_kernel, dim3(grid), dim3(256), 0, st, table, slots, hist);
+	if (n_bins < 2 || n_bins > 1024) return hipErrorInvalidValue;
+	hipLaunchKernelGGL(kc_hist_kernel, dim3(grid), dim3(256), 0, st, table, slots, hist, n_bins, min_count);
+	return hipGetLastError();
+}
+
+extern "C" hipError_t vc_launch_yak_select(const YakBloom *B, int grid, hipStream_t st)
+{
+	hipLaunchKernelGGL(yak_wanted_kernel, dim3(grid), dim3(256), 0, st, *B);
+	hipLaunchKernelGGL(yak_mintime_kernel, dim3(grid), dim3(256), 0, st, *B);
+	hipLaunchKernelGGL(yak_select_kernel, dim3(grid), dim3(256), 0, st, *B);
 	return hipGetLastError();
 }

@@ -40,7 +40,8 @@ EXPORTS = (
     "vc_gz_inflate_parallel", "vc_gz_inflate_zlib", "vc_gz_crc32",
     "vc_fasta_load", "vc_fasta_count", "vc_fasta_name", "vc_fasta_seq", "vc_fasta_data", "vc_fasta_free",
     "vc_count_candidates", "vc_set_nt4_decode",
-    "vc_kc_create", "vc_kc_set_partition", "vc_kc_slots", "vc_kc_histogram",
+    "vc_kc_create", "vc_kc_set_partition", "vc_kc_slots", "vc_kc_histogram", "vc_kc_histogram2",
+    "vc_kc_track_first", "vc_yak_bloom_select",
     "vc_synth_reads",
     "vc_debug_decode", "vc_strerror", "vc_version",
 )
@@ -128,6 +129,10 @@ def lib():
         "vc_kc_set_partition": (C.c_int, [P, C.c_uint32, C.c_uint32]),
         "vc_kc_slots": (C.c_uint64, [P]),
         "vc_kc_histogram": (C.c_int, [P, P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "vc_kc_histogram2": (C.c_int, [P, P, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint64),
+                                       C.POINTER(C.c_uint64)]),
+        "vc_kc_track_first": (C.c_int, [P, C.c_int]),
+        "vc_yak_bloom_select": (C.c_int, [P, C.c_int, C.c_int, C.c_int]),
         "vc_synth_reads": (C.c_int, [P, P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
                                      C.c_double, P, P, C.c_uint32, P]),
         "vc_debug_decode": (C.c_int, [P, C.c_size_t, P, P, C.c_uint64, P, P]),
@@ -606,13 +611,24 @@ class KmerHistogram(KmerMap):
         """Count only hash slice ``part`` of ``n_parts`` (clears the table)."""
         _ck(lib().vc_kc_set_partition(self._h, n_parts, part), "vc_kc_set_partition")
 
-    def histogram(self):
-        """(hist uint64[256], distinct, kmers): hist[c] = distinct k-mers seen
-        min(c, 255) times.  Raises VafcError(VC_EFULL) when the table ran out."""
-        hist = np.zeros(256, np.uint64)
+    def histogram(self, n_bins: int = 256, min_count: int = 1):
+        """(hist uint64[n_bins], distinct, kmers): hist[min(c, n_bins-1)] = keys
+        counted c >= min_count times (kc-c4: 256 bins; yak-count: 1024).
+        Raises VafcError(VC_EFULL) when the table ran out."""
+        hist = np.zeros(n_bins, np.uint64)
         d, km = C.c_uint64(), C.c_uint64()
-        _ck(lib().vc_kc_histogram(self._h, _ptr(hist), C.byref(d), C.byref(km)), "vc_kc_histogram")
+        _ck(lib().vc_kc_histogram2(self._h, _ptr(hist), n_bins, min_count, C.byref(d), C.byref(km)),
+            "vc_kc_histogram2")
         return hist, d.value, km.value
+
+    def track_first(self, on: bool = True) -> None:
+        """Record first-occurrence stamps (yak -b pass 1); clears the table."""
+        _ck(lib().vc_kc_track_first(self._h, 1 if on else 0), "vc_kc_track_first")
+
+    def yak_bloom_select(self, pre: int, bf_shift: int, n_hash: int) -> None:
+        """yak-count's Bloom filters replayed: keep the keys yak's pass 1 keeps,
+        counts restart at 0, later counting only touches those keys."""
+        _ck(lib().vc_yak_bloom_select(self._h, pre, bf_shift, n_hash), "vc_yak_bloom_select")
 
 
 def kc_count_file(fn: str, k: int = 31, block_size: int = 10_000_000, n_thread: int = 4,
@@ -641,6 +657,8 @@ def kc_count_file(fn: str, k: int = 31, block_size: int = 10_000_000, n_thread: 
                 return total
             cap = h.slots * 7 // 10
             n_parts = max(n_parts * 2, -(-kmers // cap) if cap else 2)
+            if n_parts > 1024:
+                raise VafcError("k-mer table too small", VC_EFULL)
     finally:
         h.close()
 
@@ -675,4 +693,86 @@ def kc_main(argv=None) -> int:
     hist = kc_count_file(args[0], k, b, t, int(os.environ.get("VAFC_KC_SLOTS", "0")),
                          int(os.environ.get("VAFC_DEVICE", "0")))
     sys.stdout.write("".join("%d\t%d\n" % (i, hist[i]) for i in range(1, 256)))
+    return 0
+
+
+def yak_count_file(fn1: str, fn2: str = None, k: int = 31, pre: int = 10, bf_shift: int = 0, n_hash: int = 4,
+                   chunk_size: int = 10_000_000, n_thread: int = 4, slots: int = 0, device: int = 0):
+    """yak_count_file + yak_ch_shrink + yak_ch_hist (yak-count.c:440-452,
+    268-288, 209-240): (hist uint64[1024], distinct k-mers after shrinking)."""
+    fn2 = fn1 if fn2 is None else fn2
+    two_pass = bf_shift > 0
+    replay = two_pass and fn1 != fn2
+    block = min(chunk_size, 0x7FFFFFFF)
+    h = KmerHistogram(k, slots, device)
+    try:
+        n_parts = 1
+        while True:
+            total, tot, kmers, full = np.zeros(1024, np.uint64), 0, 0, False
+            for part in range(n_parts):
+                h.set_partition(n_parts, part)
+                if replay:
+                    h.track_first(True)
+                h.count_file(fn1, block, n_thread)
+                h.finish()
+                try:
+                    if replay:
+                        h.yak_bloom_select(pre, bf_shift, n_hash)
+                        h.count_file(fn2, block, n_thread)
+                        h.finish()
+                    hist, d, kmers = h.histogram(1024, 2 if two_pass else 1)
+                except VafcError as e:
+                    if e.code != VC_EFULL:
+                        raise
+                    full = True
+                    break
+                total += hist
+                tot += d
+            if not full:
+                return total, tot
+            cap = h.slots * 7 // 10
+            n_parts = max(n_parts * 2, -(-kmers // cap) if cap else 2)
+            if n_parts > 1024:
+                raise VafcError("k-mer table too small", VC_EFULL)
+    finally:
+        h.close()
+
+
+def yak_main(argv=None) -> int:
+    """yak-count's main (yak-count.c:456-507): 1023 histogram lines."""
+    import getopt
+    argv = sys.argv[1:] if argv is None else argv
+    k, pre, chunk, t, b, H = 31, 10, 10_000_000, 4, 0, 4
+    try:
+        opts, args = getopt.gnu_getopt(argv, "k:p:K:t:b:H:")
+    except getopt.GetoptError:
+        opts, args = [], []
+    for o, v in opts:
+        if o == "-k":
+            k = int(v)
+        elif o == "-p":
+            pre = int(v)
+        elif o == "-K":
+            chunk = int(v)
+        elif o == "-t":
+            t = int(v)
+        elif o == "-b":
+            b = int(v)
+        elif o == "-H":
+            H = int(v)
+    if not args:
+        sys.stderr.write("Usage: yak-count [options] <in.fa> [in.fa]\nOptions:\n"
+                         "  -k INT     k-mer size [%d]\n  -p INT     prefix length [%d]\n"
+                         "  -b INT     set Bloom filter size to 2**INT bits; 0 to disable [%d]\n"
+                         "  -H INT     use INT hash functions for Bloom filter [%d]\n"
+                         "  -t INT     number of worker threads [%d]\n  -K INT     chunk size [100m]\n"
+                         "Note: -b37 is recommended for human reads\n" % (k, pre, b, H, t))
+        return 1
+    if pre < 10:
+        sys.stderr.write("ERROR: -p should be at least 10\n")
+        return 1
+    hist, tot = yak_count_file(args[0], args[1] if len(args) > 1 else None, k, pre, b, H, chunk, t,
+                               int(os.environ.get("VAFC_KC_SLOTS", "0")), int(os.environ.get("VAFC_DEVICE", "0")))
+    sys.stderr.write("[M::main] %d distinct k-mers after shrinking\n" % tot)
+    sys.stdout.write("".join("%d\t%d\n" % (i, hist[i]) for i in range(1, 1024)))
     return 0
