@@ -286,6 +286,43 @@ int vc_count_candidates(int k, const uint8_t *seq, size_t seq_bytes, const uint6
                         uint32_t *counts, int device);
 
 /* ------------------------------------------------------------------ */
+/* correlation-matrix: depth-aware Pearson between .vaf samples + tree  */
+/* (correlation-matrix.c)                      */
+/* ------------------------------------------------------------------ */
+
+typedef struct vc_vafset vc_vafset;
+int vc_vafset_create(vc_vafset **out);
+void vc_vafset_free(vc_vafset *s);
+/* load_vaf_file (correlation-matrix.c:25-90): fgets lines of at most 4095
+ * bytes, '#' and "CHR" lines skipped, rows read with the reference's 9-field
+ * sscanf conversion (vaf = field 9, depth = field 8), at most 100,000 rows
+ * (then the reference's warning on stderr); name = basename cut at the first
+ * ".vaf".  VC_EIO if the file cannot be opened (the reference exits 1). */
+int vc_vafset_add(vc_vafset *s, const char *path);
+/* A sample from arrays (n <= 100,000 rows). */
+int vc_vafset_add_arrays(vc_vafset *s, const char *name, const double *vaf, const int32_t *depth, int n);
+int vc_vafset_count(const vc_vafset *s);
+const char *vc_vafset_name(const vc_vafset *s, int i);
+int vc_vafset_snps(const vc_vafset *s, int i);
+/* calculate_correlation_matrix + pearson_correlation_depth_aware
+ * (correlation-matrix.c:94-162) on the GPU: corr[i*n + j] (n = samples, row
+ * major, symmetric, 1.0 on the diagonal) is bit-identical to the reference's
+ * double: for i < j the rows [0, rows of sample i) that have depth >=
+ * min_depth in both samples (rows past sample j's end count as vaf 0, depth
+ * 0), 0.0 below min_snps of them.  kernel_ms (may be NULL) receives the
+ * kernel time. */
+int vc_corr_matrix(const vc_vafset *s, int min_snps, int min_depth, double *corr, int device, float *kernel_ms);
+/* The same on arrays: sample i has n_snps[i] rows at vaf/depth + i*stride. */
+int vc_corr_matrix_raw(const double *vaf, const int32_t *depth, const int32_t *n_snps, int n_samples,
+                       size_t stride, int min_snps, int min_depth, double *corr, int device, float *kernel_ms);
+/* The .corr file (correlation-matrix.c:350-366): header row of names, then
+ * one row per sample, "%.6f" cells.  VC_EIO if it cannot be created. */
+int vc_corr_write(const vc_vafset *s, const double *corr, const char *path);
+/* build_tree (correlation-matrix.c:190-257): average linkage on 1 - r, the
+ * same merge order, ties and "%.4f" text.  VC_EIO if it cannot be created. */
+int vc_corr_tree(const vc_vafset *s, const double *corr, const char *path);
+
+/* ------------------------------------------------------------------ */
 /* Synthetic workload (bench / tests): the generator of vafc_synth.py,  */
 /* evaluated on the device.                                            */
 /* ------------------------------------------------------------------ */

@@ -42,6 +42,8 @@ EXPORTS = (
     "vc_count_candidates", "vc_set_nt4_decode",
     "vc_kc_create", "vc_kc_set_partition", "vc_kc_slots", "vc_kc_histogram", "vc_kc_histogram2",
     "vc_kc_track_first", "vc_yak_bloom_select",
+    "vc_vafset_create", "vc_vafset_free", "vc_vafset_add", "vc_vafset_add_arrays", "vc_vafset_count",
+    "vc_vafset_name", "vc_vafset_snps", "vc_corr_matrix", "vc_corr_matrix_raw", "vc_corr_write", "vc_corr_tree",
     "vc_synth_reads",
     "vc_debug_decode", "vc_strerror", "vc_version",
 )
@@ -133,6 +135,18 @@ def lib():
                                        C.POINTER(C.c_uint64)]),
         "vc_kc_track_first": (C.c_int, [P, C.c_int]),
         "vc_yak_bloom_select": (C.c_int, [P, C.c_int, C.c_int, C.c_int]),
+        "vc_vafset_create": (C.c_int, [C.POINTER(P)]),
+        "vc_vafset_free": (None, [P]),
+        "vc_vafset_add": (C.c_int, [P, C.c_char_p]),
+        "vc_vafset_add_arrays": (C.c_int, [P, C.c_char_p, P, P, C.c_int]),
+        "vc_vafset_count": (C.c_int, [P]),
+        "vc_vafset_name": (C.c_char_p, [P, C.c_int]),
+        "vc_vafset_snps": (C.c_int, [P, C.c_int]),
+        "vc_corr_matrix": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, C.POINTER(C.c_float)]),
+        "vc_corr_matrix_raw": (C.c_int, [P, P, P, C.c_int, C.c_size_t, C.c_int, C.c_int, P, C.c_int,
+                                         C.POINTER(C.c_float)]),
+        "vc_corr_write": (C.c_int, [P, P, C.c_char_p]),
+        "vc_corr_tree": (C.c_int, [P, P, C.c_char_p]),
         "vc_synth_reads": (C.c_int, [P, P, P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
                                      C.c_double, P, P, C.c_uint32, P]),
         "vc_debug_decode": (C.c_int, [P, C.c_size_t, P, P, C.c_uint64, P, P]),
@@ -776,3 +790,80 @@ def yak_main(argv=None) -> int:
     sys.stderr.write("[M::main] %d distinct k-mers after shrinking\n" % tot)
     sys.stdout.write("".join("%d\t%d\n" % (i, hist[i]) for i in range(1, 1024)))
     return 0
+
+
+# ---------------------------------------------------------------------------
+# correlation-matrix (correlation-matrix.c), the names
+# of the reference's functions over vc_vafset / vc_corr_* in libvafc.so
+# ---------------------------------------------------------------------------
+
+class VafSamples:
+    """The reference's sample_t array (correlation-matrix.c:11-16) as a vc_vafset."""
+
+    def __init__(self):
+        L = lib()
+        h = P()
+        _ck(L.vc_vafset_create(C.byref(h)), "vc_vafset_create")
+        self._h = h
+
+    def load_vaf_file(self, fn: str) -> None:
+        """correlation-matrix.c:25-90; VafcError(VC_EIO) if the file cannot be opened."""
+        _ck(lib().vc_vafset_add(self._h, fn.encode()), "load_vaf_file(%s)" % fn)
+
+    def add(self, name: str, vaf: np.ndarray, depth: np.ndarray) -> None:
+        vaf = np.ascontiguousarray(vaf, np.float64)
+        depth = np.ascontiguousarray(depth, np.int32)
+        _ck(lib().vc_vafset_add_arrays(self._h, name.encode(), _ptr(vaf), _ptr(depth), vaf.size), "add")
+
+    def __len__(self):
+        return lib().vc_vafset_count(self._h)
+
+    def name(self, i: int) -> str:
+        return lib().vc_vafset_name(self._h, i).decode()
+
+    def n_snps(self, i: int) -> int:
+        return lib().vc_vafset_snps(self._h, i)
+
+    def calculate_correlation_matrix(self, min_snps: int = 20, min_depth: int = 1, device: int = 0):
+        """correlation-matrix.c:146-162 on the GPU; returns (n x n float64 matrix, kernel ms)."""
+        n = len(self)
+        corr = np.zeros((n, n), np.float64)
+        ms = C.c_float()
+        _ck(lib().vc_corr_matrix(self._h, min_snps, min_depth, _ptr(corr), device, C.byref(ms)),
+            "calculate_correlation_matrix")
+        return corr, ms.value
+
+    def write_corr(self, corr: np.ndarray, fn: str) -> None:
+        corr = np.ascontiguousarray(corr, np.float64)
+        _ck(lib().vc_corr_write(self._h, _ptr(corr), fn.encode()), "write %s" % fn)
+
+    def build_tree(self, corr: np.ndarray, fn: str) -> None:
+        """correlation-matrix.c:190-257."""
+        corr = np.ascontiguousarray(corr, np.float64)
+        _ck(lib().vc_corr_tree(self._h, _ptr(corr), fn.encode()), "build_tree %s" % fn)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().vc_vafset_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def correlation_matrix_raw(vaf: np.ndarray, depth: np.ndarray, n_snps=None, min_snps: int = 20,
+                           min_depth: int = 1, device: int = 0):
+    """Pairwise depth-aware Pearson of the rows of vaf/depth ([n_samples][stride]);
+    sample i has n_snps[i] rows (default: all).  Returns (matrix, kernel ms)."""
+    vaf = np.ascontiguousarray(vaf, np.float64)
+    depth = np.ascontiguousarray(depth, np.int32)
+    n, stride = vaf.shape
+    ns = np.ascontiguousarray(np.full(n, stride) if n_snps is None else n_snps, np.int32)
+    corr = np.zeros((n, n), np.float64)
+    ms = C.c_float()
+    _ck(lib().vc_corr_matrix_raw(_ptr(vaf), _ptr(depth), _ptr(ns), n, stride, min_snps, min_depth, _ptr(corr),
+                                 device, C.byref(ms)), "vc_corr_matrix_raw")
+    return corr, ms.value
