@@ -257,6 +257,8 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel": "vc_count_reads_kernel (+ vc_count_long_kernel, empty here)",
+                "limiter": "VALU instruction issue, not HBM: the kernel's VALU-only ablation sets the floor "
+                           "(DESIGN.md section 3.1, profiles/r01_ablation_ab.log, profiles/r01_valu_rates.log)",
                 "kernel_ms": round(k_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
             },
