@@ -202,18 +202,25 @@ def main():
             with open(fq, "wb") as f:
                 for a in range(0, n, 200_000):
                     f.write(S.fastq_bytes(host[a:a + 200_000], a))
+            # -t 1, -t 4 and -t <host cores> (the box's CPU share is
+            # 16 cores), median of 3 each, the best median is the baseline
             runs = {}
-            for t in (1, 4):
-                sp, ksp, wall = cpu_reference_run(binary, pat, fq, t, os.path.join(tmp, "ref_t%d.vaf" % t), args.k)
-                runs[t] = (sp, ksp, wall)
-                log("cpu %s -t %d: %.2f Mbases/s (%.1fs)" % (kind, t, sp, wall))
+            for t in (1, 4, min(16, os.cpu_count() or 16)):
+                rs = []
+                for rep in range(3):
+                    sp, ksp, wall = cpu_reference_run(binary, pat, fq, t, os.path.join(tmp, "ref_t%d.vaf" % t),
+                                                      args.k)
+                    rs.append((sp, ksp, wall))
+                    log("cpu %s -t %d (run %d): %.2f Mbases/s (%.1fs)" % (kind, t, rep + 1, sp, wall))
+                runs[t] = sorted(rs)[1]
             best_t = max(runs, key=lambda t: runs[t][0])
             cpu = {"value": runs[best_t][0], "unit": "Mbases/sec", "cores": 3 if best_t == 1 else 3 + best_t,
                    "kind": kind,
                    "sample": "first %d reads (%d Mbases) of this workload as FASTQ, page-cached; "
-                             "reference -v Speed line; best of -t 1 (%.2f) / -t 4 (%.2f); "
+                             "reference -v Speed line, median of 3 runs per thread count; best of %s; "
                              "threads = kt_pipeline's 3 + kt_for's -t" % (
-                                 n, n * L // 1_000_000, runs[1][0], runs[4][0]),
+                                 n, n * L // 1_000_000,
+                                 " / ".join("-t %d (%.2f)" % (t, runs[t][0]) for t in sorted(runs))),
                    "kmers_per_sec": runs[best_t][1] * 1e6 if runs[best_t][1] else None}
             # live parity: the product counts the same sample from HBM
             kmap.bind_outputs(0, 0)
