@@ -25,9 +25,9 @@
 //            the higher index: the reference's zero rows past its end).
 // A pair's valid rows are lo[a] & hi[b].
 //
-// Kernel: a 256-thread block owns a tile of TA = 16 lower samples x TB = 64
+// Kernel: a 256-thread block owns a tile of TA = 32 lower samples x TB = 64
 // higher samples (tiles entirely below the diagonal exit); lane l of wave w
-// takes b = b0 + l and a = a0 + 4w .. 4w + 3, i.e. four pairs.  Rows are
+// takes b = b0 + l and a = a0 + 8w .. 8w + 7, i.e. eight pairs.  Rows are
 // staged CH = 64 at a time through LDS: the b rows transposed (row-major in
 // the lane index, conflict-free), the a rows as broadcasts (one address per
 // wave).  Each pair is a sequential scan, so there is no cross-lane
@@ -51,7 +51,10 @@
 
 namespace {
 
-constexpr int TA = 16, TB = 64, CH = 64, NT = 256, PA = TA / (NT / 64);
+#ifndef CORR_TA
+#define CORR_TA 32
+#endif
+constexpr int TA = CORR_TA, TB = 64, CH = 64, NT = 256, PA = TA / (NT / 64);
 
 struct CorrArgs {
 	const double *x;          // [n][P]
@@ -116,16 +119,20 @@ __global__ void __launch_bounds__(NT) corr_pairs_kernel(CorrArgs A)
 					const double y = xb[w * 32 + s][lb];
 #pragma unroll
 					for (int r = 0; r < PA; ++r) {
-						// branch-free: an invalid row adds +0.0, which leaves every
-						// sum as it is (a sum starts at +0.0 and never becomes -0.0
-						// under round-to-nearest; NaN / inf stay NaN / inf)
-						const bool v = (m[r] >> s) & 1u;
+						// branch-free: terms are multiplied by the row's validity
+						// f = 1.0 / 0.0.  A valid row is unchanged (x * 1 = x, so
+						// fma(x, f, s) rounds s + x once, as the reference's add); an
+						// invalid finite row adds +-0.0, which leaves every sum as it
+						// is (a sum starts at +0.0 and never becomes -0.0 under
+						// round-to-nearest).  An invalid inf / NaN row turns the sums
+						// NaN: such pairs are recounted by corr_pairs_x86_kernel.
+						const double f = (double)((m[r] >> s) & 1u);
 						const double x = xa[ag + r][w * 32 + s];
 						if (pass == 0) {
-							s1[r] = s1[r] + (v ? x : 0.0);             // correlation-matrix.c:107-112
-							s2[r] = s2[r] + (v ? y : 0.0);
+							s1[r] = __fma_rn(x, f, s1[r]);             // correlation-matrix.c:107-112
+							s2[r] = __fma_rn(y, f, s2[r]);
 						} else {
-							const double dx = v ? x - mx[r] : 0.0, dy = v ? y - my[r] : 0.0;   // :118-125
+							const double dx = (x - mx[r]) * f, dy = (y - my[r]) * f;   // :118-125
 							const double p = dx * dy, q = dx * dx, u = dy * dy;
 							pxy[r] = pxy[r] + p;
 							pxx[r] = pxx[r] + q;
