@@ -13,9 +13,10 @@
 // The output is printed with %.6f, and the tree compares distances exactly,
 // so the device reproduces the reference's doubles bit for bit: one lane per
 // pair keeps the reference's summation order; FP contraction is off; invalid
-// rows are skipped (adding 0.0 would also be exact, but skipping keeps NaN /
-// inf rows out exactly like the reference).  The host finishes each pair
-// from the device sums with the reference's formula (sqrt, epsilon branch).
+// rows contribute exactly nothing (terms times a 1.0 / 0.0 validity factor,
+// see the kernel; pairs whose sums turn NaN are recounted by the x86-NaN
+// kernel).  The host finishes each pair from the device sums with the
+// reference's formula (sqrt, epsilon branch).
 //
 // Layout (HBM): x[n_samples][P] doubles (P = rows padded to CH, zero past a
 // sample's end), and two validity bitmaps per sample, u32 words of 32 rows:
