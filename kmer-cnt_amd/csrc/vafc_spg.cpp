@@ -17,6 +17,10 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <string>
 #include <thread>
@@ -28,10 +32,155 @@
 
 struct vc_fasta {
 	std::vector<std::string> names;
-	std::vector<uint8_t> seq;
+	std::vector<uint8_t> seq;          // sequential reader
+	uint8_t *raw = nullptr;            // mapped loader: malloc'd, first touched by the copy threads
+	size_t raw_bytes = 0;
 	std::vector<uint64_t> offs;
 	std::vector<uint32_t> lens;
+	~vc_fasta() { free(raw); }
+	const uint8_t *data() const { return raw ? raw : seq.data(); }
+	size_t bytes() const { return raw ? raw_bytes : seq.size(); }
 };
+
+// Parallel load of a plain FASTA file whose records kseq reads as "header
+// line, then sequence lines up to the next line starting with '>'"
+// (kseq.h:192-232): the file is mapped, T threads find the record headers and
+// then copy each record's bytes minus the newlines straight to their final
+// place (per-segment counts, prefix sums, copies).  Anything this does not
+// restate exactly -- a first byte other than '>', a '\r', a line starting
+// with '+' or '@' (kseq's FASTQ separators) -- returns false and the caller
+// reads the file with the sequential kseq-semantics reader instead.
+static bool fasta_load_mapped(const char *path, int threads, vc_fasta *fa)
+{
+	const int fd = open(path, O_RDONLY);
+	if (fd < 0) return false;
+	struct stat sb;
+	if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode) || sb.st_size < 2) {
+		close(fd);
+		return false;
+	}
+	const size_t n = (size_t)sb.st_size;
+	void *map = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+	close(fd);
+	if (map == MAP_FAILED) return false;
+	madvise(map, n, MADV_SEQUENTIAL);
+	const uint8_t *d = (const uint8_t *)map;
+	bool ok = d[0] == '>';
+	const int T = threads;
+	// pass 1: header starts and disqualifying bytes, per thread range
+	std::vector<std::vector<size_t>> heads(T);
+	std::vector<char> bad(T, 0);
+	auto range = [&](int t, size_t &a, size_t &b) {
+		a = n * (size_t)t / (size_t)T;
+		b = n * (size_t)(t + 1) / (size_t)T;
+	};
+	if (ok) {
+		std::vector<std::thread> th;
+		for (int t = 0; t < T; ++t)
+			th.emplace_back([&, t] {
+				size_t a, b;
+				range(t, a, b);
+				if (memchr(d + a, '\r', b - a)) {
+					bad[t] = 1;
+					return;
+				}
+				if (t == 0) heads[t].push_back(0);
+				// line starts in [a, b): positions p with d[p - 1] == '\n'
+				const uint8_t *p = a ? d + a - 1 : d;
+				const uint8_t *e = d + b - 1;     // a newline at b - 1 starts a line at b (next range)
+				while (p < e && (p = (const uint8_t *)memchr(p, '\n', (size_t)(e - p))) != nullptr) {
+					const uint8_t c = p[1];
+					if (c == '>') heads[t].push_back((size_t)(p + 1 - d));
+					else if (c == '+' || c == '@') {
+						bad[t] = 1;
+						return;
+					}
+					++p;
+				}
+			});
+		for (auto &x : th) x.join();
+		for (int t = 0; t < T; ++t) ok = ok && !bad[t];
+	}
+	if (!ok) {
+		munmap(map, n);
+		return false;
+	}
+	// records: header [h, he), body [he + 1, next header)
+	std::vector<size_t> hs;
+	for (auto &v : heads) hs.insert(hs.end(), v.begin(), v.end());
+	const size_t R = hs.size();
+	std::vector<size_t> bs(R), be(R);
+	fa->names.reserve(R);
+	for (size_t r = 0; r < R; ++r) {
+		const uint8_t *nl = (const uint8_t *)memchr(d + hs[r], '\n', n - hs[r]);
+		const size_t he = nl ? (size_t)(nl - d) : n;
+		size_t q = hs[r] + 1;                    // name: up to the first isspace byte (kseq KS_SEP_SPACE)
+		while (q < he && !(d[q] == ' ' || d[q] == '\t' || d[q] == '\v' || d[q] == '\f')) ++q;
+		fa->names.emplace_back((const char *)d + hs[r] + 1, q - hs[r] - 1);
+		bs[r] = he < n ? he + 1 : n;
+		be[r] = r + 1 < R ? hs[r + 1] : n;
+	}
+	// segments: the pieces of the bodies inside each thread's range
+	struct Seg { size_t rec, a, b, len, out; };
+	std::vector<std::vector<Seg>> segs(T);
+	for (int t = 0; t < T; ++t) {
+		size_t a, b;
+		range(t, a, b);
+		for (size_t r = 0; r < R; ++r) {
+			const size_t x = bs[r] > a ? bs[r] : a, y = be[r] < b ? be[r] : b;
+			if (x < y) segs[t].push_back({r, x, y, 0, 0});
+		}
+	}
+	auto run = [&](auto fn) {
+		std::vector<std::thread> th;
+		for (int t = 0; t < T; ++t) th.emplace_back([&, t] { fn(t); });
+		for (auto &x : th) x.join();
+	};
+	run([&](int t) {                            // pass 2a: sequence bytes per segment
+		for (Seg &s : segs[t]) {
+			size_t nl = 0;
+			for (const uint8_t *p = d + s.a, *e = d + s.b; (p = (const uint8_t *)memchr(p, '\n', (size_t)(e - p)));
+			     ++p)
+				++nl;
+			s.len = s.b - s.a - nl;
+		}
+	});
+	fa->lens.assign(R, 0);
+	fa->offs.assign(R, 0);
+	size_t total = 0;
+	for (int t = 0; t < T; ++t)                 // segments are in file order
+		for (Seg &s : segs[t]) fa->lens[s.rec] += (uint32_t)s.len;
+	for (size_t r = 0; r < R; ++r) {
+		fa->offs[r] = total;
+		total += fa->lens[r];
+	}
+	std::vector<size_t> cur(fa->offs.begin(), fa->offs.end());
+	for (int t = 0; t < T; ++t)
+		for (Seg &s : segs[t]) {
+			s.out = cur[s.rec];
+			cur[s.rec] += s.len;
+		}
+	// no zero fill: the copy threads touch every page first, in parallel
+	fa->raw = (uint8_t *)malloc(total ? total : 1);
+	if (!fa->raw) throw std::bad_alloc();
+	fa->raw_bytes = total;
+	uint8_t *o = fa->raw;
+	run([&](int t) {                            // pass 2b: copy without the newlines
+		for (const Seg &s : segs[t]) {
+			uint8_t *w = o + s.out;
+			const uint8_t *p = d + s.a, *e = d + s.b;
+			while (p < e) {
+				const uint8_t *q = (const uint8_t *)memchr(p, '\n', (size_t)(e - p));
+				const size_t l = (size_t)((q ? q : e) - p);
+				memcpy(w, p, l);
+				w += l;
+				p += l + (q ? 1 : 0);
+			}
+		}
+	});
+	munmap(map, n);
+	return true;
+}
 
 // load_fasta (snp-pattern-gen.c:67-103): every record, kseq semantics, until
 // the first kseq_read < 0
@@ -43,11 +192,38 @@ extern "C" int vc_fasta_load(const char *path, vc_fasta **out)
 	const char *te = getenv("VAFC_THREADS");
 	int threads = te && atoi(te) > 0 ? atoi(te) : (int)std::thread::hardware_concurrency();
 	threads = threads < 1 ? 1 : (threads > 16 ? 16 : threads);
+	if (!getenv("VAFC_FASTA_SEQUENTIAL")) {    // test knob: force the sequential reader
+		vc_fasta *fa = new (std::nothrow) vc_fasta;
+		if (!fa) return VC_ENOMEM;
+		bool done = false;
+		try {
+			done = fasta_load_mapped(path, threads, fa);
+		} catch (...) {
+			delete fa;
+			return VC_ENOMEM;
+		}
+		if (done) {
+			*out = fa;
+			return VC_OK;
+		}
+		delete fa;
+	}
 	if (!rd.open_parallel(path, threads)) return VC_EIO;
 	rd.keep_names(true);
 	vc_fasta *fa = new (std::nothrow) vc_fasta;
 	if (!fa) return VC_ENOMEM;
 	try {
+		// a plain file's sequence bytes never exceed its size: reserve once
+		// instead of growing a genome-sized vector by doubling (each growth
+		// copies everything loaded so far)
+		struct stat sb;
+		uint8_t magic[2] = {0, 0};
+		FILE *fp = fopen(path, "rb");
+		if (fp) {
+			const bool gz = fread(magic, 1, 2, fp) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+			if (!gz && fstat(fileno(fp), &sb) == 0 && S_ISREG(sb.st_mode)) fa->seq.reserve((size_t)sb.st_size);
+			fclose(fp);
+		}
 		int ret;
 		while ((ret = rd.next()) >= 0) {
 			fa->names.emplace_back(rd.name(), rd.name_len());
@@ -74,15 +250,15 @@ extern "C" const uint8_t *vc_fasta_seq(const vc_fasta *fa, int i, uint32_t *len)
 {
 	if (!fa || i < 0 || (size_t)i >= fa->names.size()) return nullptr;
 	if (len) *len = fa->lens[(size_t)i];
-	return fa->seq.data() + fa->offs[(size_t)i];
+	return fa->data() + fa->offs[(size_t)i];
 }
 
 extern "C" int vc_fasta_data(const vc_fasta *fa, const uint8_t **seq, size_t *bytes, const uint64_t **offs,
                              const uint32_t **lens)
 {
 	if (!fa) return VC_EINVAL;
-	if (seq) *seq = fa->seq.data();
-	if (bytes) *bytes = fa->seq.size();
+	if (seq) *seq = fa->data();
+	if (bytes) *bytes = fa->bytes();
 	if (offs) *offs = fa->offs.data();
 	if (lens) *lens = fa->lens.data();
 	return VC_OK;

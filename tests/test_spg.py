@@ -33,6 +33,51 @@ def test_fasta_loader_on_fuzzed_records(tmp_path):
         assert vafc.load_fasta(p) == O.fasta_records(p), seed
 
 
+def _plain_fasta(rng, n_rec):
+    """FASTA the mapped loader takes (first byte '>', no CR, no line starting
+    with '+'/'@'): ragged and empty lines, empty records, '>' inside lines,
+    tabs/spaces/\\v/\\f in headers, NUL and high bytes, no final newline."""
+    alpha = np.frombuffer(b"ACGTNacgtn>\x00\xc1RYSW", np.uint8)
+    out = []
+    for r in range(n_rec):
+        head = b">" + rng.choice([b"chr%d" % r, b"c%d\tdesc x" % r, b"s%d d\x0bv" % r, b"", b"r%d\x0cff" % r])
+        out.append(head + b"\n")
+        for _ in range(int(rng.integers(0, 6))):
+            line = alpha[rng.integers(0, len(alpha), int(rng.integers(0, 90)))].tobytes()
+            if line[:1] in (b">",):
+                line = b"A" + line
+            out.append(line + b"\n")
+    data = b"".join(out)
+    return data[:-1] if rng.random() < 0.5 and data.endswith(b"\n") else data
+
+
+@pytest.mark.parametrize("threads", ["1", "3", "16"])
+def test_fasta_mapped_loader_matches_oracle(tmp_path, threads, monkeypatch):
+    """The parallel mapped loader (plain FASTA) against the oracle's kseq
+    restatement, and against the sequential reader, for thread counts that
+    cut records and lines at every kind of place."""
+    import vafc
+    import oracle as O
+    monkeypatch.setenv("VAFC_THREADS", threads)
+    for seed in range(12):
+        rng = np.random.default_rng(900 + seed)
+        p = str(tmp_path / ("m%d.fa" % seed))
+        with open(p, "wb") as f:
+            f.write(_plain_fasta(rng, int(rng.integers(1, 40))))
+        got = vafc.load_fasta(p)
+        assert got == O.fasta_records(p), seed
+        monkeypatch.setenv("VAFC_FASTA_SEQUENTIAL", "1")
+        assert vafc.load_fasta(p) == got, seed
+        monkeypatch.delenv("VAFC_FASTA_SEQUENTIAL")
+    # tiny files (fewer bytes than threads) and the fallback triggers
+    for i, data in enumerate([b">a\nAC", b">\n", b">x\nAC\r\nGT\n", b">x\nAC\n+\nII\n", b"AC\n>x\nGG\n",
+                              b">x\nAC\n@y\nGG\n", b">a\n>b\nA\n>c"]):
+        p = str(tmp_path / ("t%d.fa" % i))
+        with open(p, "wb") as f:
+            f.write(data)
+        assert vafc.load_fasta(p) == O.fasta_records(p), data
+
+
 ERROR_CASES = [c for c in SPG_CASES if c["exit"] != 0]
 RUN_CASES = [c for c in SPG_CASES if c["exit"] == 0]
 
