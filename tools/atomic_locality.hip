@@ -39,6 +39,15 @@ __global__ void k_bucket(unsigned long long *t, uint64_t n, uint32_t sbits, uint
 	}
 }
 
+// 32-bit counters, random order (same slot layout, low word of the count)
+__global__ void k_random32(unsigned int *t, uint64_t n, uint32_t sbits)
+{
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t s = mix(i) >> (64 - sbits);
+		atomicAdd(&t[4 * s + 2], 1u);
+	}
+}
+
 int main()
 {
 	const uint32_t sbits = 29;                 // 2^29 slots x 16 B = 8.6 GB (kc_bench's table)
@@ -58,6 +67,12 @@ int main()
 		hipEventSynchronize(e1);
 		hipEventElapsedTime(&ms, e0, e1);
 		printf("random order            %8.2f ms  %.2f G atomics/s\n", ms, n / ms / 1e6);
+		hipEventRecord(e0);
+		hipLaunchKernelGGL(k_random32, dim3(grid), dim3(block), 0, 0, (unsigned int *)t, n, sbits);
+		hipEventRecord(e1);
+		hipEventSynchronize(e1);
+		hipEventElapsedTime(&ms, e0, e1);
+		printf("random order, 32-bit    %8.2f ms  %.2f G atomics/s\n", ms, n / ms / 1e6);
 		for (uint32_t bb : {4u, 6u, 8u, 10u}) {
 			hipEventRecord(e0);
 			hipLaunchKernelGGL(k_bucket, dim3(grid), dim3(block), 0, 0, t, n, sbits, bb);
