@@ -28,6 +28,7 @@
 
 #include "vafc.h"
 #include "vafc_fastq.h"
+#include "vafc_gzip.h"
 #include "vafc_internal.h"
 
 struct vc_fasta {
@@ -42,7 +43,8 @@ struct vc_fasta {
 	size_t bytes() const { return raw ? raw_bytes : seq.size(); }
 };
 
-// Parallel load of a plain FASTA file whose records kseq reads as "header
+// Parallel load of a FASTA file (plain, or gzip through the parallel
+// inflater into memory) whose records kseq reads as "header
 // line, then sequence lines up to the next line starting with '>'"
 // (kseq.h:192-232): the file is mapped, T threads find the record headers and
 // then copy each record's bytes minus the newlines straight to their final
@@ -50,6 +52,8 @@ struct vc_fasta {
 // restate exactly -- a first byte other than '>', a '\r', a line starting
 // with '+' or '@' (kseq's FASTQ separators) -- returns false and the caller
 // reads the file with the sequential kseq-semantics reader instead.
+static bool fasta_parse_buffer(const uint8_t *d, size_t n, int threads, vc_fasta *fa);
+
 static bool fasta_load_mapped(const char *path, int threads, vc_fasta *fa)
 {
 	const int fd = open(path, O_RDONLY);
@@ -60,11 +64,61 @@ static bool fasta_load_mapped(const char *path, int threads, vc_fasta *fa)
 		return false;
 	}
 	const size_t n = (size_t)sb.st_size;
+	uint8_t magic[2] = {0, 0};
+	if (pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b) {
+		// gzip: the parallel inflater (vafc_gzip.h, gzread's output) into memory,
+		// then the same parallel parse
+		close(fd);
+		VcGzParallel *g = vc_gzp_open(path, threads, 0);
+		if (!g) return false;
+		size_t cap = n * 4 + (1u << 20), len = 0;
+		uint8_t *buf = (uint8_t *)malloc(cap);
+		bool ok = buf != nullptr;
+		while (ok) {
+			const uint8_t *p;
+			const int64_t got = vc_gzp_span(g, &p, (size_t)1 << 30);
+			if (got <= 0) break;
+			if (len + (size_t)got > cap) {
+				size_t nc = cap * 2;
+				while (nc < len + (size_t)got) nc *= 2;
+				uint8_t *nb = (uint8_t *)realloc(buf, nc);
+				if (!nb) {
+					ok = false;
+					break;
+				}
+				buf = nb;
+				cap = nc;
+			}
+			memcpy(buf + len, p, (size_t)got);
+			len += (size_t)got;
+		}
+		vc_gzp_close(g);
+		try {
+			ok = ok && len >= 2 && fasta_parse_buffer(buf, len, threads, fa);
+		} catch (...) {
+			free(buf);
+			throw;
+		}
+		free(buf);
+		return ok;
+	}
 	void *map = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
 	close(fd);
 	if (map == MAP_FAILED) return false;
 	madvise(map, n, MADV_SEQUENTIAL);
-	const uint8_t *d = (const uint8_t *)map;
+	bool ok;
+	try {
+		ok = fasta_parse_buffer((const uint8_t *)map, n, threads, fa);
+	} catch (...) {
+		munmap(map, n);
+		throw;
+	}
+	munmap(map, n);
+	return ok;
+}
+
+static bool fasta_parse_buffer(const uint8_t *d, size_t n, int threads, vc_fasta *fa)
+{
 	bool ok = d[0] == '>';
 	const int T = threads;
 	// pass 1: header starts and disqualifying bytes, per thread range
@@ -101,10 +155,7 @@ static bool fasta_load_mapped(const char *path, int threads, vc_fasta *fa)
 		for (auto &x : th) x.join();
 		for (int t = 0; t < T; ++t) ok = ok && !bad[t];
 	}
-	if (!ok) {
-		munmap(map, n);
-		return false;
-	}
+	if (!ok) return false;
 	// records: header [h, he), body [he + 1, next header)
 	std::vector<size_t> hs;
 	for (auto &v : heads) hs.insert(hs.end(), v.begin(), v.end());
@@ -178,7 +229,6 @@ static bool fasta_load_mapped(const char *path, int threads, vc_fasta *fa)
 			}
 		}
 	});
-	munmap(map, n);
 	return true;
 }
 

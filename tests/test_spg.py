@@ -69,6 +69,18 @@ def test_fasta_mapped_loader_matches_oracle(tmp_path, threads, monkeypatch):
         monkeypatch.setenv("VAFC_FASTA_SEQUENTIAL", "1")
         assert vafc.load_fasta(p) == got, seed
         monkeypatch.delenv("VAFC_FASTA_SEQUENTIAL")
+        # the same genome gzipped (two members for odd seeds): inflated in
+        # memory, then the same parallel parse
+        import gzip
+        with open(p, "rb") as f:
+            raw = f.read()
+        pz = p + ".gz"
+        with open(pz, "wb") as f:
+            if seed % 2:
+                f.write(gzip.compress(raw[: len(raw) // 2]) + gzip.compress(raw[len(raw) // 2:]))
+            else:
+                f.write(gzip.compress(raw, 6))
+        assert vafc.load_fasta(pz) == got, seed
     # tiny files (fewer bytes than threads) and the fallback triggers
     for i, data in enumerate([b">a\nAC", b">\n", b">x\nAC\r\nGT\n", b">x\nAC\n+\nII\n", b"AC\n>x\nGG\n",
                               b">x\nAC\n@y\nGG\n", b">a\n>b\nA\n>c"]):
