@@ -299,6 +299,13 @@ void vc_vafset_free(vc_vafset *s);
  * (then the reference's warning on stderr); name = basename cut at the first
  * ".vaf".  VC_EIO if the file cannot be opened (the reference exits 1). */
 int vc_vafset_add(vc_vafset *s, const char *path);
+/* The same for n files read by n_threads threads: files are appended in
+ * order up to the first one that cannot be opened (*n_added = its index,
+ * VC_EIO; VC_OK if all were); truncated[i] = 1 where the 100,000-row cap was
+ * hit, for the caller to print the reference's warning in file order
+ * (load_vaf_file prints it while loading, correlation-matrix.c:70-73). */
+int vc_vafset_add_many(vc_vafset *s, const char *const *paths, int n, int n_threads, int *n_added,
+                       uint8_t *truncated);
 /* A sample from arrays (n <= 100,000 rows). */
 int vc_vafset_add_arrays(vc_vafset *s, const char *name, const double *vaf, const int32_t *depth, int n);
 int vc_vafset_count(const vc_vafset *s);

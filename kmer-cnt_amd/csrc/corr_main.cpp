@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "vafc.h"
@@ -71,12 +72,21 @@ int main(int argc, char **argv)
 		fprintf(stderr, "Error: failed to allocate memory\n");
 		return 1;
 	}
-	for (int i = 0; i < n; ++i) {
-		if (vc_vafset_add(set, argv[optind + i]) != VC_OK) {
-			fprintf(stderr, "Error: failed to load %s\n", argv[optind + i]);
-			return 1;
-		}
+	// files are read in parallel; the messages come out in file order, as the
+	// reference's sequential loop prints them (correlation-matrix.c:329-335)
+	std::vector<uint8_t> truncated(n, 0);
+	int added = 0;
+	const int lrc = vc_vafset_add_many(set, (const char *const *)(argv + optind), n,
+	                                   (int)std::thread::hardware_concurrency() < 16
+	                                       ? (int)std::thread::hardware_concurrency() : 16,
+	                                   &added, truncated.data());
+	for (int i = 0; i < added; ++i) {
+		if (truncated[i]) fprintf(stderr, "Warning: too many SNPs (max %d), truncating\n", 100000);
 		fprintf(stderr, "[M::main] Loaded %s: %d SNPs\n", vc_vafset_name(set, i), vc_vafset_snps(set, i));
+	}
+	if (lrc != VC_OK) {
+		fprintf(stderr, "Error: failed to load %s\n", argv[optind + added]);
+		return 1;
 	}
 	fprintf(stderr, "[M::main] Computing correlation matrix...\n");
 	std::vector<double> corr((size_t)n * n);

@@ -41,7 +41,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <new>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -249,19 +251,20 @@ extern "C" int vc_vafset_snps(const vc_vafset *s, int i)
 	return s && i >= 0 && i < (int)s->name.size() ? (int)s->x[i].size() : VC_EINVAL;
 }
 
-extern "C" int vc_vafset_add(vc_vafset *s, const char *path)
+// One .vaf file; *truncated = the 100,000-row cap was hit (the caller prints
+// the reference's warning).  false if the file cannot be opened.
+static bool vaf_load_one(const char *path, std::string &nm, std::vector<double> &x, std::vector<int32_t> &d,
+                         bool &truncated)
 {
-	if (!s || !path) return VC_EINVAL;
+	truncated = false;
 	FILE *fp = fopen(path, "r");
-	if (!fp) return VC_EIO;
+	if (!fp) return false;
 	// sample name: basename, at most 255 bytes, cut at the first ".vaf"
 	const char *base = strrchr(path, '/');
-	std::string nm(base ? base + 1 : path);
+	nm.assign(base ? base + 1 : path);
 	if (nm.size() > 255) nm.resize(255);
 	const size_t cut = nm.find(".vaf");
 	if (cut != std::string::npos) nm.resize(cut);
-	std::vector<double> x;
-	std::vector<int32_t> d;
 	char line[CORR_LINE];
 	while (fgets(line, sizeof line, fp)) {          // lines past 4095 bytes arrive in pieces, as there
 		if (line[0] == '#' || strncmp(line, "CHR", 3) == 0) continue;
@@ -272,17 +275,60 @@ extern "C" int vc_vafset_add(vc_vafset *s, const char *path)
 		           &v) != 9)
 			continue;
 		if (x.size() >= CORR_CAP) {
-			fprintf(stderr, "Warning: too many SNPs (max %d), truncating\n", CORR_CAP);
+			truncated = true;
 			break;
 		}
 		x.push_back(v);
 		d.push_back(tot);
 	}
 	fclose(fp);
+	return true;
+}
+
+extern "C" int vc_vafset_add(vc_vafset *s, const char *path)
+{
+	if (!s || !path) return VC_EINVAL;
+	std::string nm;
+	std::vector<double> x;
+	std::vector<int32_t> d;
+	bool trunc;
+	if (!vaf_load_one(path, nm, x, d, trunc)) return VC_EIO;
+	if (trunc) fprintf(stderr, "Warning: too many SNPs (max %d), truncating\n", CORR_CAP);
 	s->name.push_back(nm);
 	s->x.push_back(std::move(x));
 	s->d.push_back(std::move(d));
 	return VC_OK;
+}
+
+extern "C" int vc_vafset_add_many(vc_vafset *s, const char *const *paths, int n, int n_threads, int *n_added,
+                                  uint8_t *truncated)
+{
+	if (!s || n < 0 || (n && (!paths || !n_added || !truncated))) return VC_EINVAL;
+	std::vector<std::string> nm(n);
+	std::vector<std::vector<double>> x(n);
+	std::vector<std::vector<int32_t>> d(n);
+	std::vector<char> ok(n, 0), tr(n, 0);
+	std::atomic<int> next(0);
+	const int T = n_threads < 1 ? 1 : (n_threads > 64 ? 64 : n_threads);
+	std::vector<std::thread> th;
+	for (int t = 0; t < T && t < n; ++t)
+		th.emplace_back([&] {
+			for (int i; (i = next.fetch_add(1)) < n;) {
+				bool trunc = false;
+				ok[i] = vaf_load_one(paths[i], nm[i], x[i], d[i], trunc);
+				tr[i] = trunc;
+			}
+		});
+	for (auto &t : th) t.join();
+	int i = 0;
+	for (; i < n && ok[i]; ++i) {                  // in order, up to the first file that failed
+		truncated[i] = (uint8_t)tr[i];
+		s->name.push_back(std::move(nm[i]));
+		s->x.push_back(std::move(x[i]));
+		s->d.push_back(std::move(d[i]));
+	}
+	*n_added = i;
+	return i == n ? VC_OK : VC_EIO;
 }
 
 extern "C" int vc_vafset_add_arrays(vc_vafset *s, const char *name, const double *vaf, const int32_t *depth, int n)

@@ -42,7 +42,8 @@ EXPORTS = (
     "vc_count_candidates", "vc_set_nt4_decode",
     "vc_kc_create", "vc_kc_set_partition", "vc_kc_slots", "vc_kc_histogram", "vc_kc_histogram2",
     "vc_kc_track_first", "vc_yak_bloom_select",
-    "vc_vafset_create", "vc_vafset_free", "vc_vafset_add", "vc_vafset_add_arrays", "vc_vafset_count",
+    "vc_vafset_create", "vc_vafset_free", "vc_vafset_add", "vc_vafset_add_many", "vc_vafset_add_arrays",
+    "vc_vafset_count",
     "vc_vafset_name", "vc_vafset_snps", "vc_corr_matrix", "vc_corr_matrix_raw", "vc_corr_write", "vc_corr_tree",
     "vc_synth_reads",
     "vc_debug_decode", "vc_strerror", "vc_version",
@@ -138,6 +139,7 @@ def lib():
         "vc_vafset_create": (C.c_int, [C.POINTER(P)]),
         "vc_vafset_free": (None, [P]),
         "vc_vafset_add": (C.c_int, [P, C.c_char_p]),
+        "vc_vafset_add_many": (C.c_int, [P, P, C.c_int, C.c_int, C.POINTER(C.c_int), P]),
         "vc_vafset_add_arrays": (C.c_int, [P, C.c_char_p, P, P, C.c_int]),
         "vc_vafset_count": (C.c_int, [P]),
         "vc_vafset_name": (C.c_char_p, [P, C.c_int]),
