@@ -812,6 +812,18 @@ class VafSamples:
         """correlation-matrix.c:25-90; VafcError(VC_EIO) if the file cannot be opened."""
         _ck(lib().vc_vafset_add(self._h, fn.encode()), "load_vaf_file(%s)" % fn)
 
+    def load_vaf_files(self, fns, n_threads: int = 8) -> list:
+        """load_vaf_file over many files, read by n_threads threads and appended
+        in order (vc_vafset_add_many).  Returns, per file added, whether the
+        100,000-row cap truncated it.  VafcError(VC_EIO) at the first file that
+        cannot be opened; the files before it stay added."""
+        arr = (C.c_char_p * len(fns))(*[f.encode() for f in fns])
+        trunc = np.zeros(max(len(fns), 1), np.uint8)
+        added = C.c_int(0)
+        rc = lib().vc_vafset_add_many(self._h, C.cast(arr, P), len(fns), n_threads, C.byref(added), _ptr(trunc))
+        _ck(rc, "load_vaf_files(%s)" % (fns[added.value] if rc and added.value < len(fns) else ""))
+        return [bool(t) for t in trunc[: added.value]]
+
     def add(self, name: str, vaf: np.ndarray, depth: np.ndarray) -> None:
         vaf = np.ascontiguousarray(vaf, np.float64)
         depth = np.ascontiguousarray(depth, np.int32)

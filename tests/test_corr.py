@@ -184,6 +184,28 @@ def test_loader_names_and_truncation(work):
     assert "[M::main] Loaded messy: %d SNPs\n" % S.n_snps(3) in CASES["messy"]["stderr"]
 
 
+@pytest.mark.parametrize("threads", [1, 3, 16])
+def test_loader_parallel_matches_sequential(work, threads):
+    """vc_vafset_add_many: same samples, in file order, as one vc_vafset_add
+    per file; truncation flags per file; stops at the first unopenable file
+    with the ones before it added."""
+    import vafc
+    fns = [os.path.join(work, f) for f in ("t/other.vaf.vaf", "_big/big.vaf", "e/messy.vaf", "t/noext",
+                                           "e/empty.vaf", "_big/big.vaf", "e/messy.vaf")]
+    A, B = vafc.VafSamples(), vafc.VafSamples()
+    for fn in fns:
+        A.load_vaf_file(fn)
+    assert B.load_vaf_files(fns, threads) == [False, True, False, False, False, True, False]
+    assert [(A.name(i), A.n_snps(i)) for i in range(len(A))] == [(B.name(i), B.n_snps(i)) for i in range(len(B))]
+    C_ = vafc.VafSamples()
+    with pytest.raises(vafc.VafcError) as e:
+        C_.load_vaf_files(fns[:3] + ["/nonexistent/x.vaf"] + fns[3:], threads)
+    assert e.value.code == vafc.VC_EIO and len(C_) == 3
+    assert [C_.name(i) for i in range(3)] == ["other", "big", "messy"]
+    for S in (A, B, C_):
+        S.close()
+
+
 # --- GPU ---------------------------------------------------------------------
 
 @pytest.mark.gpu
