@@ -139,6 +139,34 @@ int vc_kernel_ms(vc_ctx *ctx, float *ms);
 int vc_table_info(const vc_ctx *ctx, uint64_t *n_keys, uint64_t *slots, uint64_t *filter_bytes);
 
 /* ------------------------------------------------------------------ */
+/* Multi-GPU counter -- the reference counts all     */
+/* files into one set of counters in one process (vaf-counter.c:473-477,*/
+/* 647-650) and writes them once (:653-681).                           */
+/* ------------------------------------------------------------------ */
+
+#define VC_MAX_SHARDS 64
+
+/* A counter with one shard per entry of devices[0..n_devices): each shard
+ * holds a replica of the static table and its own counts on its device (a
+ * device may repeat: several shards on one GPU).  Host reads given to
+ * vc_count_block / vc_count_file are dealt to the shards batch by batch,
+ * round robin (the -b block loop and its stop rule still run once, in file
+ * order); vc_count_device counts on shard 0 only.  vc_finish reduces the
+ * shards -- same-device shards summed on their device, then one RCCL reduce
+ * (ncclSum of the u32 counts and the u64 k-mer tally) to shard 0 over xGMI,
+ * librccl.so.1 loaded on first use -- and returns the totals, bit-identical
+ * to a single device counting everything (u32 sums wrap like the
+ * reference's counters).  vc_reset / vc_set_nt4_decode apply to every shard;
+ * vc_bind_outputs, vc_device_counts, timing and vc_table_info to shard 0.
+ * n_devices == 1 is vc_create. */
+int vc_create_multi(vc_ctx **out, int k, const uint64_t *keys, const uint32_t *vals, size_t n_keys,
+                    uint32_t n_patterns, const int *devices, int n_devices);
+/* Shards of a counter (1 for vc_create), and shard i's device and the host
+ * batches it has counted so far. */
+int vc_shard_count(const vc_ctx *ctx);
+int vc_shard_info(const vc_ctx *ctx, int i, int *device, uint64_t *batches);
+
+/* ------------------------------------------------------------------ */
 /* Whole-file pass -- replaces count_fastq_kmers (vaf-counter.c:550).  */
 /* ------------------------------------------------------------------ */
 

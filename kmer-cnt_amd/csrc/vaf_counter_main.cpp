@@ -3,7 +3,9 @@
 // Drop-in for the reference CLI (vaf-counter.c:584-738): same options
 // "k:p:o:t:b:v" (options may follow the input files), same usage text, same
 // stderr messages, same .vaf output and exit codes.  The counting phase runs
-// on the GPU (device: $VAFC_DEVICE, default 0).
+// on the GPU (device: $VAFC_DEVICE, default 0), or on several: $VAFC_DEVICES
+// is a comma-separated device list, one shard per entry (vc_create_multi:
+// batches dealt round robin, one RCCL reduce before the .vaf is written).
 #include <getopt.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -56,7 +58,19 @@ int main(int argc, char *argv[])
 		return 1;
 	}
 	const char *dev_env = getenv("VAFC_DEVICE");
-	const int device = dev_env ? atoi(dev_env) : 0;
+	std::vector<int> devices(1, dev_env ? atoi(dev_env) : 0);
+	if (const char *ds = getenv("VAFC_DEVICES")) {
+		std::vector<int> v;
+		for (const char *p = ds; *p;) {
+			char *e = nullptr;
+			const long d = strtol(p, &e, 10);
+			if (e == p) break;
+			v.push_back((int)d);
+			p = *e == ',' ? e + 1 : e;
+			if (*e != ',') break;
+		}
+		if (!v.empty()) devices = v;
+	}
 
 	const double t_start = now_s();
 	fprintf(stderr, "[M::%s] Loading patterns...\n", "main");
@@ -88,7 +102,7 @@ int main(int argc, char *argv[])
 		fprintf(stderr, "[W::%s] Warning: %d k-mer collisions detected. "
 		        "Some patterns may have overlapping k-mers.\n", "create_combined_kmer_map", n_coll);
 	vc_ctx *ctx = nullptr;
-	rc = vc_create(&ctx, k, keys, vals, n_keys, (uint32_t)n, device);
+	rc = vc_create_multi(&ctx, k, keys, vals, n_keys, (uint32_t)n, devices.data(), (int)devices.size());
 	vc_free(keys);
 	vc_free(vals);
 	if (rc == VC_OK) rc = vc_reserve_file_ingest(ctx, n_thread);   // reader buffers, outside the counting timer
@@ -183,6 +197,8 @@ int main(int argc, char *argv[])
 		fprintf(stderr, "\nOptimizations:\n");
 		fprintf(stderr, "  SIMD:                  MI355X HIP (gfx950), LDS prefilter %llu KiB, device table %llu slots\n",
 		        (unsigned long long)(fbytes >> 10), (unsigned long long)tslots);
+		if (devices.size() > 1)
+			fprintf(stderr, "  Shards:                %d (RCCL reduce of the counts)\n", (int)devices.size());
 		fprintf(stderr, "  Threads:               %d workers\n", n_thread);
 		fprintf(stderr, "==============================\n");
 	}

@@ -4,12 +4,16 @@
 //   device ctx    static key table + LDS prefilter in HBM, counts, streams
 //   count_block   host block -> pinned staging -> H2D -> kernels (async)
 //   count_file    count_fastq_kmers: block loop + kseq reader  vaf-counter.c:482-582
+//   shards        one table replica + counts per GPU, host batches dealt
+//                 round robin, one RCCL reduce before the writer  
 //   write_vaf     .vaf writer                                  vaf-counter.c:653-681
 //
 // Nothing here computes counts on the CPU: every k-mer goes through the HIP
 // kernels in vafc_kernels.hip, and any HIP failure is returned as VC_EHIP.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <limits.h>
 #include <math.h>
@@ -19,6 +23,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <unordered_map>
 #include <vector>
 
@@ -257,7 +262,19 @@ struct vc_ctx {
 	bool timing = false, timed = false;
 	hipEvent_t t0 = nullptr, t1 = nullptr;
 	struct Kc *kc = nullptr;               // histogram mode (vc_kc_create)
+	// multi-GPU (vc_create_multi): this ctx is shard 0; rep[i - 1] is shard i
+	std::vector<vc_ctx *> rep;
+	std::vector<int> lead;                 // per shard: the first shard on the same device
+	std::vector<ncclComm_t> comms;         // one rank per distinct device, rank 0 = shard 0
+	std::vector<int> comm_shard;           // the shard each rank reduces
+	uint64_t rr = 0;                       // host batches dealt so far (round robin)
+	uint64_t batches = 0;                  // batches counted by this shard (vc_shard_info)
 };
+
+static inline int n_shards(const vc_ctx *c) { return 1 + (int)c->rep.size(); }
+static inline vc_ctx *shard_at(vc_ctx *c, int i) { return i == 0 ? c : c->rep[(size_t)i - 1]; }
+// The shard that takes the next host batch.
+static inline vc_ctx *next_shard(vc_ctx *c) { return shard_at(c, (int)(c->rr++ % (uint64_t)n_shards(c))); }
 
 // kc-c4 histogram mode: the device hash table and its bookkeeping
 struct Kc {
@@ -409,9 +426,14 @@ static void free_slot(Slot &s)
 	s.pending = false;
 }
 
+static void rccl_comms_destroy(vc_ctx *c);
+
 extern "C" void vc_destroy(vc_ctx *c)
 {
 	if (!c) return;
+	rccl_comms_destroy(c);
+	for (vc_ctx *r : c->rep) vc_destroy(r);
+	c->rep.clear();
 	(void)hipSetDevice(c->dev);
 	if (c->st) (void)hipStreamSynchronize(c->st);
 	for (auto &s : c->slot) {
@@ -549,6 +571,7 @@ extern "C" int vc_set_nt4_decode(vc_ctx *c, int on)
 {
 	if (!c) return VC_EINVAL;
 	c->nt4 = on ? 1 : 0;
+	for (vc_ctx *r : c->rep) r->nt4 = c->nt4;
 	return VC_OK;
 }
 
@@ -604,6 +627,7 @@ static int slot_submit(vc_ctx *c, Slot &s, size_t bytes, uint64_t n_reads)
 		if (rc != VC_OK) return rc;
 		HIPCK(hipEventRecord(s.done, c->st));
 		s.pending = true;
+		++c->batches;
 	}
 	c->cur ^= 1;
 	return VC_OK;
@@ -614,9 +638,10 @@ extern "C" int vc_count_block(vc_ctx *c, const uint8_t *seq, size_t seq_bytes, c
 {
 	if (!c || (n_reads && (!seq || !offs || !lens))) return VC_EINVAL;
 	if (n_reads == 0) return VC_OK;
-	HIPCK(hipSetDevice(c->dev));
 	for (uint64_t i = 0; i < n_reads; ++i)
 		if (offs[i] + lens[i] > seq_bytes) return VC_EINVAL;
+	c = next_shard(c);
+	HIPCK(hipSetDevice(c->dev));
 	Slot *s;
 	int rc = slot_acquire(c, &s);
 	if (rc == VC_OK) rc = slot_reserve(*s, seq_bytes, n_reads);
@@ -627,9 +652,15 @@ extern "C" int vc_count_block(vc_ctx *c, const uint8_t *seq, size_t seq_bytes, c
 	return slot_submit(c, *s, seq_bytes, n_reads);
 }
 
+static int reduce_shards(vc_ctx *c);
+
 extern "C" int vc_finish(vc_ctx *c, uint32_t *counts, uint64_t *kmers)
 {
 	if (!c) return VC_EINVAL;
+	if (!c->rep.empty()) {
+		int rc = reduce_shards(c);
+		if (rc != VC_OK) return rc;
+	}
 	HIPCK(hipSetDevice(c->dev));
 	HIPCK(hipStreamSynchronize(c->st));
 	HIPCK(hipDeviceSynchronize());
@@ -668,6 +699,10 @@ extern "C" int vc_reset(vc_ctx *c)
 	}
 	HIPCK(hipMemsetAsync(c->d_counts, 0, 2 * (size_t)c->n_patterns * sizeof(uint32_t), c->st));
 	HIPCK(hipMemsetAsync(c->d_tally, 0, sizeof(unsigned long long), c->st));
+	for (vc_ctx *r : c->rep) {
+		int rc = vc_reset(r);
+		if (rc != VC_OK) return rc;
+	}
 	return VC_OK;
 }
 
@@ -710,6 +745,183 @@ extern "C" int vc_table_info(const vc_ctx *c, uint64_t *n_keys, uint64_t *slots,
 }
 
 // ---------------------------------------------------------------------------
+// multi-GPU shards.  The reference counts every block of
+// every file into one set of u32 counters (vaf-counter.c:473-477, files in
+// order :647-650) and writes them once (:653-681).  Here each shard (one per
+// entry of the device list) holds a replica of the static table and its own
+// counts; host batches are dealt round robin over the shards, the block loop
+// and its stop rule still run once, in file order, on the host.  vc_finish
+// reduces: shards sharing a device are summed on it (vc_shard_add_kernel),
+// then one RCCL reduce (sum) of the per-device vectors to shard 0 over xGMI.
+// u32 addition modulo 2^32 commutes, so the result is bit-identical to one
+// device counting everything.
+// ---------------------------------------------------------------------------
+
+namespace {
+
+// RCCL, loaded on first use so that single-GPU users do not need it.
+struct RcclApi {
+	bool tried = false, ok = false;
+	decltype(&ncclCommInitAll) comm_init_all = nullptr;
+	decltype(&ncclCommDestroy) comm_destroy = nullptr;
+	decltype(&ncclReduce) reduce = nullptr;
+	decltype(&ncclGroupStart) group_start = nullptr;
+	decltype(&ncclGroupEnd) group_end = nullptr;
+	decltype(&ncclGetErrorString) error_string = nullptr;
+};
+RcclApi g_rccl;
+std::mutex g_rccl_mu;
+
+const RcclApi *rccl()
+{
+	std::lock_guard<std::mutex> lk(g_rccl_mu);
+	if (g_rccl.tried) return g_rccl.ok ? &g_rccl : nullptr;
+	g_rccl.tried = true;
+	void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+	if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+	if (!h) {
+		fprintf(stderr, "[E::vafc] cannot load RCCL: %s\n", dlerror());
+		return nullptr;
+	}
+	RcclApi &R = g_rccl;
+	R.comm_init_all = (decltype(R.comm_init_all))dlsym(h, "ncclCommInitAll");
+	R.comm_destroy = (decltype(R.comm_destroy))dlsym(h, "ncclCommDestroy");
+	R.reduce = (decltype(R.reduce))dlsym(h, "ncclReduce");
+	R.group_start = (decltype(R.group_start))dlsym(h, "ncclGroupStart");
+	R.group_end = (decltype(R.group_end))dlsym(h, "ncclGroupEnd");
+	R.error_string = (decltype(R.error_string))dlsym(h, "ncclGetErrorString");
+	R.ok = R.comm_init_all && R.comm_destroy && R.reduce && R.group_start && R.group_end && R.error_string;
+	if (!R.ok) fprintf(stderr, "[E::vafc] RCCL lacks the symbols vafc needs\n");
+	return R.ok ? &R : nullptr;
+}
+
+} // namespace
+
+#define NCCK(R, call)                                                                               \
+	do {                                                                                            \
+		ncclResult_t e_ = (call);                                                                   \
+		if (e_ != ncclSuccess) {                                                                    \
+			fprintf(stderr, "[E::vafc] %s failed: %s (%s:%d)\n", #call, (R)->error_string(e_),      \
+			        __FILE__, __LINE__);                                                            \
+			return VC_EHIP;                                                                         \
+		}                                                                                           \
+	} while (0)
+
+static void rccl_comms_destroy(vc_ctx *c)
+{
+	if (c->comms.empty()) return;
+	const RcclApi *R = rccl();
+	if (R)
+		for (ncclComm_t m : c->comms) (void)R->comm_destroy(m);
+	c->comms.clear();
+	c->comm_shard.clear();
+}
+
+extern "C" int vc_create_multi(vc_ctx **out, int k, const uint64_t *keys, const uint32_t *vals, size_t n_keys,
+                               uint32_t n_patterns, const int *devices, int n_devices)
+{
+	if (!out || !devices || n_devices < 1 || n_devices > VC_MAX_SHARDS) return VC_EINVAL;
+	*out = nullptr;
+	vc_ctx *c = nullptr;
+	int rc = vc_create(&c, k, keys, vals, n_keys, n_patterns, devices[0]);
+	if (rc != VC_OK) return rc;
+	c->lead.assign(1, 0);
+	for (int i = 1; i < n_devices; ++i) {
+		vc_ctx *r = nullptr;
+		if ((rc = vc_create(&r, k, keys, vals, n_keys, n_patterns, devices[i])) != VC_OK) {
+			vc_destroy(c);
+			return rc;
+		}
+		c->rep.push_back(r);
+		int l = i;
+		for (int j = 0; j < i; ++j)
+			if (devices[j] == devices[i]) {
+				l = j;
+				break;
+			}
+		c->lead.push_back(l);
+	}
+	if (n_devices > 1) {
+		// one RCCL rank per distinct device; rank 0 is shard 0 (the reduce root)
+		const RcclApi *R = rccl();
+		if (!R) {
+			vc_destroy(c);
+			return VC_EHIP;
+		}
+		std::vector<int> devs;
+		for (int i = 0; i < n_devices; ++i)
+			if (c->lead[(size_t)i] == i) {
+				devs.push_back(devices[i]);
+				c->comm_shard.push_back(i);
+			}
+		c->comms.assign(devs.size(), nullptr);
+		const ncclResult_t e = R->comm_init_all(c->comms.data(), (int)devs.size(), devs.data());
+		if (e != ncclSuccess) {
+			fprintf(stderr, "[E::vafc] ncclCommInitAll over %d devices failed: %s\n", (int)devs.size(),
+			        R->error_string(e));
+			c->comms.clear();
+			vc_destroy(c);
+			return VC_EHIP;
+		}
+	}
+	*out = c;
+	return VC_OK;
+}
+
+// All shards' counts (and k-mer tallies) into shard 0; the other shards
+// restart from zero, so the sum over shards is unchanged and vc_finish may be
+// called again.
+static int reduce_shards(vc_ctx *c)
+{
+	const int N = n_shards(c);
+	const size_t n = 2 * (size_t)c->n_patterns;
+	for (int i = 0; i < N; ++i) {   // every batch counted
+		vc_ctx *sh = shard_at(c, i);
+		HIPCK(hipSetDevice(sh->dev));
+		HIPCK(hipStreamSynchronize(sh->st));
+	}
+	for (int i = 0; i < N; ++i) {   // same-device shards into the device's first shard
+		const int l = c->lead[(size_t)i];
+		if (l == i) continue;
+		vc_ctx *L = shard_at(c, l), *S = shard_at(c, i);
+		HIPCK(hipSetDevice(L->dev));
+		HIPCK(vc_launch_shard_add(L->d_counts, S->d_counts, n, L->d_tally, S->d_tally, L->st));
+	}
+	const RcclApi *R = rccl();
+	if (!R) return VC_EHIP;
+	NCCK(R, R->group_start());
+	for (size_t j = 0; j < c->comms.size(); ++j) {
+		vc_ctx *L = shard_at(c, c->comm_shard[j]);
+		if (n) NCCK(R, R->reduce(L->d_counts, L->d_counts, n, ncclUint32, ncclSum, 0, c->comms[j], L->st));
+		NCCK(R, R->reduce(L->d_tally, L->d_tally, 1, ncclUint64, ncclSum, 0, c->comms[j], L->st));
+	}
+	NCCK(R, R->group_end());
+	for (size_t j = 1; j < c->comms.size(); ++j) {   // non-root ranks restart from zero
+		vc_ctx *L = shard_at(c, c->comm_shard[j]);
+		HIPCK(hipSetDevice(L->dev));
+		HIPCK(hipMemsetAsync(L->d_counts, 0, n * sizeof(uint32_t), L->st));
+		HIPCK(hipMemsetAsync(L->d_tally, 0, sizeof(unsigned long long), L->st));
+	}
+	for (size_t j = 0; j < c->comms.size(); ++j) {
+		vc_ctx *L = shard_at(c, c->comm_shard[j]);
+		HIPCK(hipSetDevice(L->dev));
+		HIPCK(hipStreamSynchronize(L->st));
+	}
+	return VC_OK;
+}
+
+extern "C" int vc_shard_count(const vc_ctx *c) { return c ? n_shards(c) : 0; }
+
+extern "C" int vc_shard_info(const vc_ctx *c, int i, int *device, uint64_t *batches)
+{
+	if (!c || i < 0 || i >= n_shards(c)) return VC_EINVAL;
+	const vc_ctx *sh = shard_at(const_cast<vc_ctx *>(c), i);
+	if (device) *device = sh->dev;
+	if (batches) *batches = sh->batches;
+	return VC_OK;
+}
+
+// ---------------------------------------------------------------------------
 // whole-file pass (count_fastq_kmers, vaf-counter.c:550-582)
 // ---------------------------------------------------------------------------
 
@@ -720,19 +932,27 @@ extern "C" int vc_table_info(const vc_ctx *c, uint64_t *n_keys, uint64_t *slots,
 namespace {
 
 // Accepted reads are written straight into a pinned slot; a full slot is
-// shipped to the device and the other slot is filled meanwhile.
+// shipped to the device and the other slot is filled meanwhile.  With several
+// shards each batch goes to the next shard (its own slots, stream and device).
 struct BatchWriter {
 	vc_ctx *c;
+	vc_ctx *sh = nullptr;         // shard of the open slot
 	Slot *s = nullptr;
-	size_t bytes = 0;
+	size_t bytes = 0, limit = VC_BATCH_BYTES;
 	uint64_t n = 0;
 	int err = VC_OK;
 
-	explicit BatchWriter(vc_ctx *ctx) : c(ctx) {}
+	explicit BatchWriter(vc_ctx *ctx) : c(ctx)
+	{
+		const char *e = getenv("VAFC_BATCH_BYTES");   // test knob: smaller batches
+		if (e && atoll(e) >= 1) limit = (size_t)atoll(e);
+	}
 
 	int open_slot()
 	{
-		int rc = slot_acquire(c, &s);
+		sh = next_shard(c);
+		if (hipSetDevice(sh->dev) != hipSuccess) return VC_EHIP;
+		int rc = slot_acquire(sh, &s);
 		if (rc == VC_OK) rc = slot_reserve(*s, VC_BATCH_BYTES, VC_BATCH_BYTES / 64);
 		bytes = 0;
 		n = 0;
@@ -741,7 +961,7 @@ struct BatchWriter {
 	int flush()
 	{
 		if (!s) return VC_OK;
-		int rc = slot_submit(c, *s, bytes, n);
+		int rc = slot_submit(sh, *s, bytes, n);
 		s = nullptr;
 		bytes = 0;
 		n = 0;
@@ -750,7 +970,7 @@ struct BatchWriter {
 	int add(const char *seq, size_t len)
 	{
 		if (!s && (err = open_slot()) != VC_OK) return err;
-		if (bytes + len > s->cap_bytes || n + 1 > s->cap_reads) {
+		if (bytes + len > s->cap_bytes || n + 1 > s->cap_reads || (n > 0 && bytes + len > limit)) {
 			if (n > 0) {
 				if ((err = flush()) != VC_OK) return err;
 				if ((err = open_slot()) != VC_OK) return err;
@@ -786,13 +1006,16 @@ double wall_now()
 
 namespace {
 
+// Slot g of the reader lives on shard g % N (slot index g / N there), so the
+// pieces of a file go round robin over the shards.
 class DeviceSink : public VcIngestSink {
 public:
-	explicit DeviceSink(vc_ctx *c) : c_(c) {}
+	explicit DeviceSink(vc_ctx *c) : c_(c), n_(n_shards(c)) {}
 	int acquire(int slot, VcSlotBuf *b) override
 	{
-		HIPCK(hipSetDevice(c_->dev));
-		Slot &s = c_->islot[(size_t)slot];
+		vc_ctx *sh;
+		Slot &s = at(slot, &sh);
+		HIPCK(hipSetDevice(sh->dev));
 		if (s.pending) {
 			HIPCK(hipEventSynchronize(s.done));
 			s.pending = false;
@@ -802,8 +1025,9 @@ public:
 	}
 	int grow(int slot, VcSlotBuf *b, size_t bytes, size_t reads, size_t used_bytes, size_t used_reads) override
 	{
-		HIPCK(hipSetDevice(c_->dev));
-		Slot &s = c_->islot[(size_t)slot];
+		vc_ctx *sh;
+		Slot &s = at(slot, &sh);
+		HIPCK(hipSetDevice(sh->dev));
 		Slot n;
 		n.done = s.done;
 		if (hipHostMalloc(&n.h_seq, bytes, hipHostMallocDefault) != hipSuccess ||
@@ -826,19 +1050,28 @@ public:
 	}
 	int submit(int slot, const VcSlotBuf &, uint64_t n, uint64_t bytes) override
 	{
-		Slot &s = c_->islot[(size_t)slot];
-		HIPCK(hipMemcpyAsync(s.d_seq, s.h_seq, bytes, hipMemcpyHostToDevice, c_->st));
-		HIPCK(hipMemcpyAsync(s.d_offs, s.h_offs, n * sizeof(uint64_t), hipMemcpyHostToDevice, c_->st));
-		HIPCK(hipMemcpyAsync(s.d_lens, s.h_lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, c_->st));
-		int rc = launch(c_, s.d_seq, bytes, s.d_offs, s.d_lens, n, c_->st);
+		vc_ctx *sh;
+		Slot &s = at(slot, &sh);
+		HIPCK(hipSetDevice(sh->dev));
+		HIPCK(hipMemcpyAsync(s.d_seq, s.h_seq, bytes, hipMemcpyHostToDevice, sh->st));
+		HIPCK(hipMemcpyAsync(s.d_offs, s.h_offs, n * sizeof(uint64_t), hipMemcpyHostToDevice, sh->st));
+		HIPCK(hipMemcpyAsync(s.d_lens, s.h_lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, sh->st));
+		int rc = launch(sh, s.d_seq, bytes, s.d_offs, s.d_lens, n, sh->st);
 		if (rc != VC_OK) return rc;
-		HIPCK(hipEventRecord(s.done, c_->st));
+		HIPCK(hipEventRecord(s.done, sh->st));
 		s.pending = true;
+		++sh->batches;
 		return VC_OK;
 	}
 
 private:
 	vc_ctx *c_;
+	int n_;
+	Slot &at(int slot, vc_ctx **sh)
+	{
+		*sh = shard_at(c_, slot % n_);
+		return (*sh)->islot[(size_t)(slot / n_)];
+	}
 	static void fill(const Slot &s, VcSlotBuf *b)
 	{
 		b->seq = s.h_seq;
@@ -860,10 +1093,25 @@ static int clamp_threads(int n) { return n < 1 ? 1 : (n > 64 ? 64 : n); }
 
 // Pinned + device buffers of the parallel reader's slots (threads + 2 slots of
 // one piece each: sequence bytes at about half a FASTQ piece, growing on
-// demand for FASTA).
+// demand for FASTA), rounded up to a multiple of the shards and spread over
+// them.  Returns the reader's slot count (> 0) or an error (< 0).
+static int reserve_ingest_slots(vc_ctx *c, size_t slots);
+
 static int reserve_ingest(vc_ctx *c, int threads)
 {
-	const size_t slots = (size_t)threads + 2;
+	const int N = n_shards(c);
+	const int slots = (threads + 2 + N - 1) / N * N;
+	for (int i = 0; i < N; ++i) {
+		vc_ctx *sh = shard_at(c, i);
+		HIPCK(hipSetDevice(sh->dev));
+		int rc = reserve_ingest_slots(sh, (size_t)(slots / N));
+		if (rc != VC_OK) return rc;
+	}
+	return slots;
+}
+
+static int reserve_ingest_slots(vc_ctx *c, size_t slots)
+{
 	if (c->islot.size() < slots) {
 		HIPCK(hipStreamSynchronize(c->st));
 		const size_t old = c->islot.size();
@@ -883,21 +1131,31 @@ static int reserve_ingest(vc_ctx *c, int threads)
 extern "C" int vc_reserve_file_ingest(vc_ctx *c, int n_threads)
 {
 	if (!c) return VC_EINVAL;
-	HIPCK(hipSetDevice(c->dev));
-	return reserve_ingest(c, clamp_threads(n_threads));
+	const int rc = reserve_ingest(c, clamp_threads(n_threads));
+	return rc < 0 ? rc : VC_OK;
 }
 
 static int count_file_parallel(vc_ctx *c, int fd, uint64_t size, int block_bases, int n_threads,
                                vc_file_stats &st)
 {
 	const int threads = clamp_threads(n_threads);
-	const int slots = threads + 2;
-	int rc = reserve_ingest(c, threads);
-	if (rc != VC_OK) return rc;
+	const int slots = reserve_ingest(c, threads);
+	if (slots < 0) return slots;
 	DeviceSink sink(c);
 	const char *pe = getenv("VAFC_INGEST_PIECE");          // test knob: piece size in bytes
 	const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : VC_PIECE_BYTES;
 	return vc_ingest_plain(fd, size, c->k, block_bases, threads, slots, piece, sink, st);
+}
+
+// Wait for every shard's queued batches.
+static int sync_shards(vc_ctx *c)
+{
+	for (int i = 0; i < n_shards(c); ++i) {
+		vc_ctx *sh = shard_at(c, i);
+		HIPCK(hipSetDevice(sh->dev));
+		HIPCK(hipStreamSynchronize(sh->st));
+	}
+	return hipSetDevice(c->dev) == hipSuccess ? VC_OK : VC_EHIP;
 }
 
 extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n_threads,
@@ -919,7 +1177,7 @@ extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n
 		if (plain && (uint64_t)sb.st_size >= min_bytes && sb.st_size > 0) {
 			int rc = count_file_parallel(c, fd, (uint64_t)sb.st_size, block_bases, n_threads, local);
 			close(fd);
-			if (rc == VC_OK) HIPCK(hipStreamSynchronize(c->st));
+			if (rc == VC_OK) rc = sync_shards(c);
 			local.seconds = wall_now() - t0;
 			if (st) *st = local;
 			return rc;
@@ -932,7 +1190,7 @@ extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n
 	int rc = vc_block_loop(rd, c->k, block_bases,
 	                    [&bw](const char *s, size_t l) { return bw.add(s, l); }, local);
 	if (rc == VC_OK) rc = bw.flush();
-	if (rc == VC_OK) HIPCK(hipStreamSynchronize(c->st));
+	if (rc == VC_OK) rc = sync_shards(c);
 	local.seconds = wall_now() - t0;
 	if (st) *st = local;
 	return rc;

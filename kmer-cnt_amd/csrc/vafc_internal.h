@@ -55,6 +55,8 @@ hipError_t vc_launch_decode(const uint8_t *seq, uint64_t seq_bytes, const uint64
 hipError_t vc_launch_synth(uint8_t *seq, uint64_t *offs, uint32_t *lens, uint64_t first,
                            uint64_t n_reads, uint32_t L, uint64_t seed, uint64_t thr,
                            const uint8_t *win, const uint8_t *dosage, uint32_t n_snp, hipStream_t st);
+hipError_t vc_launch_shard_add(uint32_t *dst, uint32_t *src, uint64_t n, unsigned long long *dst_tally,
+                               unsigned long long *src_tally, hipStream_t st);
 #ifdef __cplusplus
 }
 #endif

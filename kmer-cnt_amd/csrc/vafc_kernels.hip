@@ -101,8 +101,39 @@ __global__ void vc_synth_kernel(uint8_t *seq, uint64_t *offs, uint32_t *lens, ui
 }
 
 // ---------------------------------------------------------------------------
+// multi-shard reduction, step 1: shards that share a device are summed into
+// the device's first shard (u32 adds wrap like the reference's counters) and
+// restart from zero; the devices' sums then go through RCCL (vafc_host.cpp)
+// ---------------------------------------------------------------------------
+
+__global__ void vc_shard_add_kernel(uint32_t *dst, uint32_t *src, uint64_t n, unsigned long long *dst_tally,
+                                    unsigned long long *src_tally)
+{
+	const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	for (uint64_t i = gid; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+		dst[i] += src[i];
+		src[i] = 0u;
+	}
+	if (gid == 0) {
+		*dst_tally += *src_tally;
+		*src_tally = 0ull;
+	}
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+
+extern "C" hipError_t vc_launch_shard_add(uint32_t *dst, uint32_t *src, uint64_t n, unsigned long long *dst_tally,
+                                          unsigned long long *src_tally, hipStream_t st)
+{
+	uint64_t blocks = (n + 255) / 256;
+	if (blocks < 1) blocks = 1;
+	if (blocks > 1024) blocks = 1024;
+	hipLaunchKernelGGL(vc_shard_add_kernel, dim3((unsigned)blocks), dim3(256), 0, st, dst, src, n, dst_tally,
+	                   src_tally);
+	return hipGetLastError();
+}
 
 extern "C" hipError_t vc_launch_count(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
 {

@@ -36,7 +36,7 @@ EXPORTS = (
     "vc_write_vaf", "vc_pattern_fields", "vc_free", "vc_create", "vc_destroy",
     "vc_count_block", "vc_count_device", "vc_finish", "vc_reset", "vc_device_counts",
     "vc_bind_outputs", "vc_device_tally", "vc_stream", "vc_set_timing", "vc_kernel_ms",
-    "vc_table_info", "vc_count_file", "vc_scan_file", "vc_scan_file_parallel", "vc_scan_records", "vc_reserve_file_ingest",
+    "vc_table_info", "vc_create_multi", "vc_shard_count", "vc_shard_info", "vc_count_file", "vc_scan_file", "vc_scan_file_parallel", "vc_scan_records", "vc_reserve_file_ingest",
     "vc_gz_inflate_parallel", "vc_gz_inflate_zlib", "vc_gz_crc32",
     "vc_fasta_load", "vc_fasta_count", "vc_fasta_name", "vc_fasta_seq", "vc_fasta_data", "vc_fasta_free",
     "vc_count_candidates", "vc_set_nt4_decode",
@@ -97,6 +97,9 @@ def lib():
         "vc_free": (None, [P]),
         "vc_create": (C.c_int, [C.POINTER(P), C.c_int, P, P, C.c_size_t, C.c_uint32, C.c_int]),
         "vc_destroy": (None, [P]),
+        "vc_create_multi": (C.c_int, [C.POINTER(P), C.c_int, P, P, C.c_size_t, C.c_uint32, P, C.c_int]),
+        "vc_shard_count": (C.c_int, [P]),
+        "vc_shard_info": (C.c_int, [P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_uint64)]),
         "vc_count_block": (C.c_int, [P, P, C.c_size_t, P, P, C.c_uint64]),
         "vc_count_device": (C.c_int, [P, P, C.c_size_t, P, P, C.c_uint64, P]),
         "vc_finish": (C.c_int, [P, P, C.POINTER(C.c_uint64)]),
@@ -246,17 +249,37 @@ def load_patterns(fn: str) -> PatternDB:
 # --------------------------------------------------------------------------
 
 class KmerMap:
-    """The device-resident static key table + counts (kmer_cnt_t + pattern_t counters)."""
+    """The device-resident static key table + counts (kmer_cnt_t + pattern_t counters).
 
-    def __init__(self, k: int, keys: np.ndarray, vals: np.ndarray, n_patterns: int, device: int = 0):
+    ``devices`` (a list of device ids, repeats allowed) makes a multi-GPU
+    counter (vc_create_multi): one table replica + counts per entry, host
+    batches dealt round robin, one RCCL reduce in ``finish()``."""
+
+    def __init__(self, k: int, keys: np.ndarray, vals: np.ndarray, n_patterns: int, device: int = 0,
+                 devices=None):
         keys = np.ascontiguousarray(keys, dtype=np.uint64)
         vals = np.ascontiguousarray(vals, dtype=np.uint32)
         self.k, self.n_patterns, self.device = k, int(n_patterns), device
         h = P()
-        _ck(lib().vc_create(C.byref(h), k, _ptr(keys), _ptr(vals), keys.size, self.n_patterns, device),
-            "vc_create")
+        if devices:
+            devs = np.ascontiguousarray(devices, dtype=np.int32)
+            self.device = int(devs[0])
+            _ck(lib().vc_create_multi(C.byref(h), k, _ptr(keys), _ptr(vals), keys.size, self.n_patterns,
+                                      _ptr(devs), devs.size), "vc_create_multi")
+        else:
+            _ck(lib().vc_create(C.byref(h), k, _ptr(keys), _ptr(vals), keys.size, self.n_patterns, device),
+                "vc_create")
         self._h = h
         self.n_collisions = 0
+
+    def shards(self):
+        """[(device, host batches counted)] per shard."""
+        out = []
+        for i in range(lib().vc_shard_count(self._h)):
+            d, b = C.c_int(), C.c_uint64()
+            _ck(lib().vc_shard_info(self._h, i, C.byref(d), C.byref(b)), "vc_shard_info")
+            out.append((d.value, b.value))
+        return out
 
     # -- counting -----------------------------------------------------------
     def count_block(self, seq: np.ndarray, offs: np.ndarray, lens: np.ndarray) -> None:
@@ -323,13 +346,14 @@ class KmerMap:
             pass
 
 
-def create_combined_kmer_map(db: PatternDB, k: int, device: int = 0) -> KmerMap:
-    """create_combined_kmer_map (vaf-counter.c:198): keys -> static device table."""
+def create_combined_kmer_map(db: PatternDB, k: int, device: int = 0, devices=None) -> KmerMap:
+    """create_combined_kmer_map (vaf-counter.c:198): keys -> static device table
+    (one replica per entry of ``devices`` for a multi-GPU counter)."""
     keys, vals, coll = db.keys(k)
     if coll > 0:
         sys.stderr.write("[W::create_combined_kmer_map] Warning: %d k-mer collisions detected. "
                          "Some patterns may have overlapping k-mers.\n" % coll)
-    m = KmerMap(k, keys, vals, db.n, device)
+    m = KmerMap(k, keys, vals, db.n, device, devices)
     m.n_collisions = coll
     return m
 
@@ -523,7 +547,8 @@ def main(argv=None) -> int:
     err("[M::main] Loaded %d patterns in %.3f sec\n" % (db.n, time.time() - t))
     err("[M::main] Creating k-mer map...\n")
     try:
-        kmap = create_combined_kmer_map(db, k, int(os.environ.get("VAFC_DEVICE", "0")))
+        devs = [int(x) for x in os.environ.get("VAFC_DEVICES", "").split(",") if x.strip()]
+        kmap = create_combined_kmer_map(db, k, int(os.environ.get("VAFC_DEVICE", "0")), devs or None)
     except VafcError:
         err("Error: failed to create k-mer map\n")
         return 1

@@ -56,7 +56,7 @@ def test_shard_partition(n, world):
     assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
 
 
-def _rank_main(rank, world, port, pat, reads_path, out_path):
+def _rank_main(rank, world, port, pat, reads_path, out_path, counter="oracle"):
     import torch.distributed as dist
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -68,8 +68,17 @@ def _rank_main(rank, world, port, pat, reads_path, out_path):
     z = np.load(reads_path)
     seq, offs, lens = z["seq"], z["offs"], z["lens"]
     first, cnt = D.shard(lens.size, rank, world)
-    orc = O.Oracle(21, pattern_fn=pat)       # CPU stand-in for the per-GPU counter
-    counts, km = orc.count_reads(seq, offs[first:first + cnt], lens[first:first + cnt])
+    if counter == "hip":                     # the product's counter (GPU tests)
+        import vafc
+        db = vafc.load_patterns(pat)
+        m = vafc.create_combined_kmer_map(db, 21, device=0)
+        m.count_block(seq, offs[first:first + cnt], lens[first:first + cnt])
+        counts, km = m.finish()
+        counts = counts.copy()
+        m.close()
+    else:                                    # CPU stand-in for the per-GPU counter
+        orc = O.Oracle(21, pattern_fn=pat)
+        counts, km = orc.count_reads(seq, offs[first:first + cnt], lens[first:first + cnt])
     if rank == 0:
         counts[0] = np.uint32((int(counts[0]) + 0xFFFFFFFF) & 0xFFFFFFFF)   # force a wrap
     t = D.counts_to_tensor(counts)
@@ -81,7 +90,10 @@ def _rank_main(rank, world, port, pat, reads_path, out_path):
     dist.destroy_process_group()
 
 
-def test_gloo_allreduce_of_sharded_counts_is_bit_exact(tmp_path):
+@pytest.mark.parametrize("counter", ["oracle", pytest.param("hip", marks=pytest.mark.gpu)])
+def test_gloo_allreduce_of_sharded_counts_is_bit_exact(tmp_path, counter):
+    """Two ranks count their shards (the oracle on CPU; the HIP counter, both
+    ranks on device 0, in the GPU suite) and all-reduce over gloo."""
     import socket
     import torch.multiprocessing as mp
     import vafc_synth as S
@@ -97,7 +109,8 @@ def test_gloo_allreduce_of_sharded_counts_is_bit_exact(tmp_path):
     port = s.getsockname()[1]
     s.close()
     out = str(tmp_path / "out.npz")
-    mp.start_processes(_rank_main, args=(2, port, pat, rp, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_rank_main, args=(2, port, pat, rp, out, counter), nprocs=2, join=True,
+                       start_method="spawn")
     got = np.load(out)
     orc = O.Oracle(21, pattern_fn=pat)
     want, km = orc.count_reads(seq, offs, lens)
