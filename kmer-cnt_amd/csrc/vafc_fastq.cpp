@@ -40,10 +40,10 @@ bool VcFastqReader::open_parallel(const char *path, int threads, uint64_t chunk_
 	return true;
 }
 
-bool VcFastqReader::open_fd(int fd, uint64_t off, size_t window)
+bool VcFastqReader::open_src(VcTextSource *src, uint64_t off, size_t window)
 {
 	close();
-	fd_ = fd;
+	src_ = src;
 	foff_ = base_ = off;
 	cap_ = window;
 	buf_ = (uint8_t *)malloc(cap_);
@@ -62,7 +62,7 @@ void VcFastqReader::close()
 		buf_ = nullptr;   // not owned
 	}
 	gzp_ = nullptr;
-	fd_ = -1;
+	src_ = nullptr;
 	free(buf_);
 	buf_ = nullptr;
 }
@@ -71,8 +71,8 @@ bool VcFastqReader::refill()
 {
 	if (eof_) return false;
 	ssize_t n;
-	if (fd_ >= 0) {
-		do n = pread(fd_, buf_, cap_, (off_t)foff_); while (n < 0 && errno == EINTR);
+	if (src_) {
+		n = (ssize_t)src_->read(buf_, cap_, foff_);
 		base_ = foff_;
 		if (n > 0) foff_ += (uint64_t)n;
 	} else if (gzp_) {   // the inflater's own buffer, no copy

@@ -17,6 +17,17 @@
 
 class VcGzParallel;
 
+// Random-access view of an input text for the parallel reader
+// (vafc_ingest.h): a plain file read with pread, or a gzip stream as it is
+// being inflated.
+class VcTextSource {
+public:
+	virtual ~VcTextSource() = default;
+	// Up to n bytes at offset off into p, waiting until they exist; fewer
+	// than n only at the end of the text (or after the source was aborted).
+	virtual int64_t read(uint8_t *p, size_t n, uint64_t off) = 0;
+};
+
 class VcByteBuf {
 public:
 	char *s = nullptr;
@@ -50,10 +61,10 @@ public:
 	bool open_parallel(const char *path, int threads, uint64_t chunk_bytes = 0,
 	                   size_t window = (size_t)4 << 20);
 	bool gz_parallel() const { return gzp_ != nullptr; }
-	// Plain-file source for the parallel ingest: records from file offset
-	// `off` of an open descriptor (read with pread, the descriptor is not
-	// owned).  `off` must be where kseq would look for a record's header.
-	bool open_fd(int fd, uint64_t off, size_t window = (size_t)4 << 20);
+	// Source for the parallel ingest: records from offset `off` of a text
+	// source (not owned).  `off` must be where kseq would look for a
+	// record's header.
+	bool open_src(VcTextSource *src, uint64_t off, size_t window = (size_t)4 << 20);
 	void close();
 	int next();
 	// File offset of the next record's header character ('@' or '>'),
@@ -70,14 +81,14 @@ public:
 private:
 	gzFile fp_ = nullptr;
 	VcGzParallel *gzp_ = nullptr;   // parallel gzip source (open_parallel)
-	int fd_ = -1;                 // pread source (open_fd), not owned
-	uint64_t foff_ = 0;           // file offset of the next pread
-	uint64_t base_ = 0;           // file offset of buf_[0] (pread source)
+	VcTextSource *src_ = nullptr; // random-access source (open_src), not owned
+	uint64_t foff_ = 0;           // text offset of the next source read
+	uint64_t base_ = 0;           // text offset of buf_[0] (source reads)
 	uint8_t *buf_ = nullptr;
 	size_t cap_ = 0, b_ = 0, e_ = 0;
 	bool eof_ = false;
 	int hdr_ = 0;                 // header char already consumed, 0 if none
-	uint64_t hdr_pos_ = 0;        // its file offset (pread source)
+	uint64_t hdr_pos_ = 0;        // its text offset (source reads)
 	VcByteBuf seq_, name_;
 	bool keep_name_ = false;
 

@@ -30,6 +30,7 @@
 #include "vafc.h"
 #include "vafc_common.h"
 #include "vafc_fastq.h"
+#include "vafc_gzip.h"
 #include "vafc_ingest.h"
 #include "vafc_internal.h"
 #include "vafc_kc.h"
@@ -1147,6 +1148,19 @@ static int count_file_parallel(vc_ctx *c, int fd, uint64_t size, int block_bases
 	return vc_ingest_plain(fd, size, c->k, block_bases, threads, slots, piece, sink, st);
 }
 
+// gzip input: the text the parallel inflater produces (n_threads workers) is
+// parsed by the parallel reader's workers, fewer of them (vc_gz_parse_threads).
+static int count_file_gzip(vc_ctx *c, VcGzParallel *g, int block_bases, int n_threads, vc_file_stats &st)
+{
+	const int parsers = vc_gz_parse_threads(clamp_threads(n_threads));
+	const int slots = reserve_ingest(c, parsers);
+	if (slots < 0) return slots;
+	DeviceSink sink(c);
+	const char *pe = getenv("VAFC_INGEST_PIECE");          // test knob: piece size in bytes
+	const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : VC_PIECE_BYTES;
+	return vc_ingest_gzip(g, c->k, block_bases, parsers, slots, piece, (uint64_t)(slots + 2) * piece * 2, sink, st);
+}
+
 // Wait for every shard's queued batches.
 static int sync_shards(vc_ctx *c)
 {
@@ -1170,8 +1184,9 @@ extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n
 		if (fd < 0) return VC_EIO;
 		struct stat sb;
 		uint8_t magic[2] = {0, 0};
-		const bool plain = fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode) &&
-		                   !(pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b);
+		const bool reg = fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
+		const bool gz = reg && pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+		const bool plain = reg && !gz;
 		const char *me = getenv("VAFC_INGEST_MIN");        // test knob: smallest file for the parallel reader
 		const uint64_t min_bytes = me ? (uint64_t)atoll(me) : VC_PARALLEL_MIN_BYTES;
 		if (plain && (uint64_t)sb.st_size >= min_bytes && sb.st_size > 0) {
@@ -1183,8 +1198,20 @@ extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n
 			return rc;
 		}
 		close(fd);
+		if (gz) {   // parallel inflate + parallel parse (falls through if the inflater declines the file)
+			const char *ce = getenv("VAFC_GZ_CHUNK");            // test knob: compressed bytes per chunk
+			VcGzParallel *g = vc_gzp_open(path, clamp_threads(n_threads), ce ? (uint64_t)atoll(ce) : 0);
+			if (g) {
+				int rc = count_file_gzip(c, g, block_bases, n_threads, local);
+				vc_gzp_close(g);
+				if (rc == VC_OK) rc = sync_shards(c);
+				local.seconds = wall_now() - t0;
+				if (st) *st = local;
+				return rc;
+			}
+		}
 	}
-	VcFastqReader rd;   // gzip: inflated by n_threads workers (vafc_gzip.h)
+	VcFastqReader rd;   // small plain files, pipes, gzip the inflater declines
 	if (!rd.open_parallel(path, clamp_threads(n_threads))) return VC_EIO;
 	BatchWriter bw(c);
 	int rc = vc_block_loop(rd, c->k, block_bases,

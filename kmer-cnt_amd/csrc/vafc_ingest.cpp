@@ -10,18 +10,21 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <thread>
 #include <vector>
 
 #include "vafc_fastq.h"
+#include "vafc_gzip.h"
 
 namespace {
 
 struct Piece {
+	uint64_t j = 0;               // piece index (the ring holds `slots` pieces)
 	uint64_t a = 0, b = 0;        // nominal byte range [a, b)
 	int64_t start = -1;           // header offset parsing began at; -1: no record found
-	uint64_t end = 0;             // header offset of the first record at or past b; size at EOF
+	uint64_t end = 0;             // header offset of the first record at or past b; text size at EOF
 	bool eof = false;             // the reader hit end of input inside this piece
 	uint64_t n = 0, bytes = 0;    // accepted reads (len >= k) in the slot, their bases
 	std::vector<uint64_t> errs;   // a -2 came after this many accepted reads
@@ -42,6 +45,167 @@ ssize_t pread_full(int fd, uint8_t *p, size_t n, uint64_t off)
 	return (ssize_t)got;
 }
 
+// A plain file through pread.
+class FdSource : public VcIngestSource {
+public:
+	FdSource(int fd, uint64_t size) : fd_(fd), size_(size) {}
+	int64_t read(uint8_t *p, size_t n, uint64_t off) override { return pread_full(fd_, p, n, off); }
+	bool longer_than(uint64_t off) override { return size_ > off; }
+
+private:
+	int fd_;
+	uint64_t size_;
+};
+
+// A gzip file's text: a pump thread takes the inflater's output in order and
+// appends it to a list of blocks; readers wait for the bytes they need.
+// Blocks wholly before the release point are freed.  The pump stays at most
+// about `window` bytes ahead of the release point unless a reader waits for
+// more (a record longer than the window must still be read).
+class GzSource : public VcIngestSource {
+public:
+	GzSource(VcGzParallel *g, uint64_t window) : g_(g), window_(window) { pump_ = std::thread([this] { pump(); }); }
+	~GzSource() override
+	{
+		abort();
+		pump_.join();
+		for (Block *b : blocks_) {
+			free(b->p);
+			delete b;
+		}
+	}
+	int64_t read(uint8_t *p, size_t n, uint64_t off) override
+	{
+		std::vector<std::pair<const uint8_t *, size_t>> seg;
+		size_t got = 0;
+		{
+			std::unique_lock<std::mutex> lk(mu_);
+			wait_for(lk, off + n);
+			if (end_ <= off) return 0;
+			got = (size_t)(end_ - off < n ? end_ - off : n);
+			// the blocks holding [off, off + got); never freed under a reader
+			// (release points lie before every offset still to be read)
+			size_t need = got;
+			uint64_t pos = off;
+			for (Block *b : blocks_) {
+				if (!need) break;
+				if (b->off + b->len <= pos) continue;
+				const size_t from = (size_t)(pos - b->off);
+				const size_t take = b->len - from < need ? b->len - from : need;
+				seg.emplace_back(b->p + from, take);
+				pos += take;
+				need -= take;
+			}
+		}
+		size_t at = 0;
+		for (auto &sg : seg) {
+			memcpy(p + at, sg.first, sg.second);
+			at += sg.second;
+		}
+		return (int64_t)got;
+	}
+	bool longer_than(uint64_t off) override
+	{
+		std::unique_lock<std::mutex> lk(mu_);
+		wait_for(lk, off + 1);
+		return end_ > off;
+	}
+	void release(uint64_t off) override
+	{
+		std::lock_guard<std::mutex> lk(mu_);
+		if (off <= rel_) return;
+		rel_ = off;
+		while (blocks_.size() > 1 && blocks_.front()->off + blocks_.front()->len <= rel_) {
+			free(blocks_.front()->p);
+			delete blocks_.front();
+			blocks_.pop_front();
+		}
+		room_.notify_all();
+	}
+	void abort() override
+	{
+		std::lock_guard<std::mutex> lk(mu_);
+		aborted_ = true;
+		data_.notify_all();
+		room_.notify_all();
+	}
+
+private:
+	struct Block {
+		uint64_t off = 0;      // text offset of p[0]
+		size_t len = 0, cap = 0;
+		uint8_t *p = nullptr;
+	};
+	VcGzParallel *g_;
+	uint64_t window_;
+	std::thread pump_;
+	std::mutex mu_;
+	std::condition_variable data_, room_;
+	std::deque<Block *> blocks_;
+	uint64_t end_ = 0, rel_ = 0;   // bytes produced; release point
+	int waiting_ = 0;              // readers waiting for bytes not produced yet
+	bool eof_ = false, aborted_ = false;
+
+	void wait_for(std::unique_lock<std::mutex> &lk, uint64_t want)
+	{
+		while (end_ < want && !eof_ && !aborted_) {
+			++waiting_;
+			room_.notify_all();
+			data_.wait(lk);
+			--waiting_;
+		}
+	}
+	void pump()
+	{
+		for (;;) {
+			{
+				std::unique_lock<std::mutex> lk(mu_);
+				room_.wait(lk, [&] { return aborted_ || end_ - rel_ < window_ || waiting_ > 0; });
+				if (aborted_) break;
+			}
+			const uint8_t *q = nullptr;
+			const int64_t n = vc_gzp_span(g_, &q, (size_t)8 << 20);
+			if (n <= 0) break;
+			// the tail block's bytes past end_ are invisible to readers, so
+			// they are written without the lock; a new block is linked under it
+			size_t done = 0;
+			while (done < (size_t)n) {
+				Block *t = nullptr;
+				{
+					std::lock_guard<std::mutex> lk(mu_);
+					t = blocks_.empty() ? nullptr : blocks_.back();
+				}
+				if (!t || t->len == t->cap) {
+					Block *nb = new Block;
+					nb->cap = (size_t)n - done > ((size_t)8 << 20) ? (size_t)n - done : ((size_t)8 << 20);
+					nb->p = (uint8_t *)malloc(nb->cap);
+					if (!nb->p) {
+						delete nb;
+						std::lock_guard<std::mutex> lk(mu_);
+						aborted_ = true;   // out of memory: readers see a short text
+						data_.notify_all();
+						return;
+					}
+					std::lock_guard<std::mutex> lk(mu_);
+					nb->off = end_;
+					blocks_.push_back(nb);
+					t = nb;
+				}
+				const size_t take = t->cap - t->len < (size_t)n - done ? t->cap - t->len : (size_t)n - done;
+				memcpy(t->p + t->len, q + done, take);
+				std::lock_guard<std::mutex> lk(mu_);
+				t->len += take;
+				end_ += take;
+				done += take;
+				data_.notify_all();
+			}
+		}
+		std::lock_guard<std::mutex> lk(mu_);
+		eof_ = true;
+		data_.notify_all();
+	}
+};
+
 const uint8_t *find_nl(const uint8_t *p, const uint8_t *e)
 {
 	return p < e ? (const uint8_t *)memchr(p, '\n', (size_t)(e - p)) : nullptr;
@@ -52,15 +216,15 @@ const uint8_t *find_nl(const uint8_t *p, const uint8_t *e)
 // same length, then '@' or end of input.  FASTA: any line starting with '>'
 // or '@' (kseq ends a FASTA record at either).  Only a guess: the caller
 // checks it against the previous piece's end.
-int64_t guess_record(int fd, uint64_t size, uint64_t a, bool fasta, std::vector<uint8_t> &tmp)
+int64_t guess_record(VcTextSource &src, uint64_t a, bool fasta, std::vector<uint8_t> &tmp)
 {
 	const uint64_t from = a - 1;
-	const size_t want = (size_t)((size - from) < ((uint64_t)1 << 20) ? (size - from) : ((uint64_t)1 << 20));
+	const size_t want = (size_t)1 << 20;
 	tmp.resize(want);
-	const ssize_t got = pread_full(fd, tmp.data(), want, from);
+	const int64_t got = src.read(tmp.data(), want, from);
 	if (got < 2) return -1;
 	const uint8_t *s = tmp.data(), *e = s + got;
-	const bool at_eof = from + (uint64_t)got >= size;
+	const bool at_eof = (size_t)got < want;   // a short read ends at the end of the text
 	for (const uint8_t *p = s + 1; p < e; ++p) {
 		if (p[-1] != '\n') {
 			p = find_nl(p, e);
@@ -91,21 +255,21 @@ int64_t guess_record(int fd, uint64_t size, uint64_t a, bool fasta, std::vector<
 
 // Parse records whose header lies in [start, P.b) (kseq semantics from a
 // record boundary) into the piece's slot.
-int parse_piece(int fd, uint64_t size, uint64_t start, int k, int slot, VcIngestSink &sink,
-                VcFastqReader &rd, Piece &P)
+int parse_piece(VcTextSource &src, uint64_t start, int k, int slot, VcIngestSink &sink, VcFastqReader &rd,
+                Piece &P)
 {
 	P.start = (int64_t)start;
 	P.n = P.bytes = 0;
 	P.errs.clear();
 	P.eof = false;
 	P.end = start;
-	if (!rd.open_fd(fd, start, (size_t)1 << 20)) return VC_ENOMEM;
+	if (!rd.open_src(&src, start, (size_t)1 << 20)) return VC_ENOMEM;
 	size_t used = 0;
 	for (;;) {
 		const int64_t h = rd.peek_header();
 		if (h < 0) {
 			P.eof = true;
-			P.end = size;
+			P.end = UINT64_MAX;   // nothing follows
 			break;
 		}
 		if ((uint64_t)h >= P.b) {
@@ -115,7 +279,7 @@ int parse_piece(int fd, uint64_t size, uint64_t start, int k, int slot, VcIngest
 		const int ret = rd.next();
 		if (ret == -1) {
 			P.eof = true;
-			P.end = size;
+			P.end = UINT64_MAX;
 			break;
 		}
 		if (ret == -2) {
@@ -194,31 +358,31 @@ static double ing_now()
 	return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, int slots,
-                    uint64_t piece_bytes, VcIngestSink &sink, vc_file_stats &st)
+int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int slots, uint64_t piece_bytes,
+                   VcIngestSink &sink, vc_file_stats &st)
 {
 	const bool prof = getenv("VAFC_INGEST_PROFILE") != nullptr;
 	double t_wait = 0, t_submit = 0, t_reparse = 0;
 	std::atomic<uint64_t> t_parse_us{0}, t_slotwait_us{0};
 	const double t_begin = ing_now();
 	if (threads < 1 || slots < threads + 1 || piece_bytes < 2) return VC_EINVAL;
-	if (size == 0) {   // empty input: three empty blocks, nothing counted
-		return VC_OK;
-	}
+	if (!src.longer_than(0)) return VC_OK;   // empty input: three empty blocks, nothing counted
 	bool fasta = false;
 	{
 		VcFastqReader rd;
-		if (!rd.open_fd(fd, 0, (size_t)1 << 16)) return VC_ENOMEM;
+		if (!rd.open_src(&src, 0, (size_t)1 << 16)) return VC_ENOMEM;
 		const int64_t h = rd.peek_header();
 		if (h < 0) return VC_OK;      // no record at all
 		uint8_t c = 0;
-		if (pread_full(fd, &c, 1, (uint64_t)h) == 1) fasta = c == '>';
+		if (src.read(&c, 1, (uint64_t)h) == 1) fasta = c == '>';
 	}
-	const uint64_t np = (size + piece_bytes - 1) / piece_bytes;
-	std::vector<Piece> pcs((size_t)np);
+	// piece j lives in pcs[j % slots] and fills slot j % slots; a worker takes
+	// piece j once piece j - slots has been released by the main thread
+	std::vector<Piece> pcs((size_t)slots);
 	std::mutex mu;
 	std::condition_variable cv;
-	uint64_t released = 0;            // pieces whose slot the main thread is done with
+	uint64_t released = 0;            // pieces the main thread is done with
+	uint64_t n_pieces = UINT64_MAX;   // known once a worker finds its piece past the end
 	bool abort = false;
 	std::atomic<uint64_t> next{0};
 
@@ -227,22 +391,28 @@ int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, 
 		std::vector<uint8_t> tmp;
 		for (;;) {
 			const uint64_t j = next.fetch_add(1);
-			if (j >= np) return;
-			Piece &P = pcs[(size_t)j];
 			const double w0 = prof ? ing_now() : 0;
 			{
 				std::unique_lock<std::mutex> lk(mu);
-				cv.wait(lk, [&] { return abort || j < (uint64_t)slots || released + slots > j; });
-				if (abort) return;
+				cv.wait(lk, [&] { return abort || released + (uint64_t)slots > j; });
+				if (abort || j >= n_pieces) return;
+			}
+			if (!src.longer_than(j * piece_bytes)) {
+				std::lock_guard<std::mutex> lk(mu);
+				if (j < n_pieces) n_pieces = j;
+				cv.notify_all();
+				return;
 			}
 			const double w1 = prof ? ing_now() : 0;
 			const int slot = (int)(j % (uint64_t)slots);
+			Piece &P = pcs[(size_t)slot];
+			P.j = j;
 			P.a = j * piece_bytes;
-			P.b = P.a + piece_bytes < size ? P.a + piece_bytes : size;
+			P.b = P.a + piece_bytes;
 			int rc = sink.acquire(slot, &P.buf);
 			if (rc == VC_OK) {
-				const int64_t g = j == 0 ? 0 : guess_record(fd, size, P.a, fasta, tmp);
-				if (g >= 0) rc = parse_piece(fd, size, (uint64_t)g, k, slot, sink, rd, P);
+				const int64_t g = j == 0 ? 0 : guess_record(src, P.a, fasta, tmp);
+				if (g >= 0) rc = parse_piece(src, (uint64_t)g, k, slot, sink, rd, P);
 				else P.start = -1;
 			}
 			if (prof) {
@@ -256,29 +426,30 @@ int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, 
 			cv.notify_all();
 		}
 	};
-	const int nt = (uint64_t)threads < np ? threads : (int)np;
 	std::vector<std::thread> pool;
-	for (int t = 0; t < nt; ++t) pool.emplace_back(worker);
+	for (int t = 0; t < threads; ++t) pool.emplace_back(worker);
 
 	int rc = VC_OK;
 	BlockState S;
 	uint64_t expect = 0;              // where the next record's header is
+	uint64_t np = 0;
 	VcFastqReader rd;
-	for (uint64_t j = 0; j < np; ++j) {
-		Piece &P = pcs[(size_t)j];
+	for (uint64_t j = 0;; ++j) {
+		const int slot = (int)(j % (uint64_t)slots);
+		Piece &P = pcs[(size_t)slot];
 		const double m0 = prof ? ing_now() : 0;
 		{
 			std::unique_lock<std::mutex> lk(mu);
-			cv.wait(lk, [&] { return P.ready; });
+			cv.wait(lk, [&] { return (P.ready && P.j == j) || n_pieces <= j; });
+			if (!(P.ready && P.j == j)) break;   // past the end of the text
 		}
-		const double m1 = prof ? ing_now() : 0;
-		if (prof) t_wait += m1 - m0;
-		const int slot = (int)(j % (uint64_t)slots);
+		np = j + 1;
+		if (prof) t_wait += ing_now() - m0;
 		if (rc == VC_OK) rc = P.rc;
 		if (rc == VC_OK && !S.stopped && P.b > expect) {
 			if (P.start < 0 || (uint64_t)P.start != expect) { // a wrong guess: parse from the true boundary
 				const double r0 = prof ? ing_now() : 0;
-				rc = parse_piece(fd, size, expect, k, slot, sink, rd, P);
+				rc = parse_piece(src, expect, k, slot, sink, rd, P);
 				if (prof) t_reparse += ing_now() - r0;
 			}
 			if (rc == VC_OK) {
@@ -292,14 +463,21 @@ int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, 
 				}
 			}
 		}
+		// later reads start at the next piece's guess (one byte before it) or
+		// at the next record boundary
+		const uint64_t nxt = (j + 1) * piece_bytes - 1;
+		src.release(expect < nxt ? expect : nxt);
+		const bool done = rc != VC_OK || S.stopped;
 		{
 			std::lock_guard<std::mutex> lk(mu);
+			P.ready = false;
 			released = j + 1;
-			if (rc != VC_OK) abort = true;
+			if (done) abort = true;
 			cv.notify_all();
 		}
-		if (rc != VC_OK) break;   // workers see abort; pieces not yet taken are dropped
+		if (done) break;   // workers see abort; pieces not yet taken are dropped
 	}
+	src.abort();   // wake workers still reading pieces that are no longer needed
 	for (auto &t : pool) t.join();
 	if (prof)
 		fprintf(stderr, "[ingest] %llu pieces, %d threads: total %.3f s; main: wait %.3f submit %.3f reparse %.3f; "
@@ -307,11 +485,25 @@ int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, 
 		        ing_now() - t_begin, t_wait, t_submit, t_reparse, t_parse_us.load() * 1e-6,
 		        t_slotwait_us.load() * 1e-6);
 	if (rc == VC_OK && !S.stopped) {
-		// the input ended inside a record the last piece never reached (cannot
-		// happen: the last piece parses to end of input) -- be explicit anyway
+		// the text ended inside a record the last piece never reached (cannot
+		// happen: the last piece parses to the end of the text) -- be explicit
 		rc = VC_EINVAL;
 	}
 	return rc;
+}
+
+int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, int slots,
+                    uint64_t piece_bytes, VcIngestSink &sink, vc_file_stats &st)
+{
+	FdSource src(fd, size);
+	return vc_ingest_text(src, k, block_bases, threads, slots, piece_bytes, sink, st);
+}
+
+int vc_ingest_gzip(VcGzParallel *g, int k, int block_bases, int threads, int slots, uint64_t piece_bytes,
+                   uint64_t window_bytes, VcIngestSink &sink, vc_file_stats &st)
+{
+	GzSource src(g, window_bytes);
+	return vc_ingest_text(src, k, block_bases, threads, slots, piece_bytes, sink, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -409,18 +601,31 @@ extern "C" int vc_scan_file_parallel(const char *path, int k, int block_bases, i
 	uint8_t magic[2] = {0, 0};
 	if (pread_full(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b) {
 		// gzip: n_threads inflate workers (piece_bytes compressed bytes per
-		// chunk), the block loop over the inflated stream in this thread
+		// chunk), the inflated text parsed by vc_gz_parse_threads workers in
+		// pieces of $VAFC_INGEST_PIECE (default 16 MB) -- vc_count_file's reader
 		close(fd);
-		VcFastqReader rd;
-		if (!rd.open_parallel(path, n_threads, piece_bytes)) return VC_EIO;
-		size_t nb = 0, nr = 0;
-		const int rc = vc_block_loop(rd, k, block_bases, [&](const char *q, size_t l) {
-			if (seq_out && nb + l <= seq_cap) memcpy(seq_out + nb, q, l);
-			if (lens_out && nr < lens_cap) lens_out[nr] = (uint32_t)l;
-			nb += l;
-			++nr;
-			return VC_OK;
-		}, local);
+		int rc;
+		VcGzParallel *g = vc_gzp_open(path, n_threads, piece_bytes);
+		if (g) {
+			const char *pe = getenv("VAFC_INGEST_PIECE");
+			const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : ((uint64_t)16 << 20);
+			const int parsers = vc_gz_parse_threads(n_threads);
+			HostSink sink(parsers + 2, piece, seq_out, seq_cap, lens_out, lens_cap);
+			rc = vc_ingest_gzip(g, k, block_bases, parsers, parsers + 2, piece, (uint64_t)(parsers + 4) * piece * 2,
+			                    sink, local);
+			vc_gzp_close(g);
+		} else {   // the inflater declines the file: gzread, one thread
+			VcFastqReader rd;
+			if (!rd.open(path)) return VC_EIO;
+			size_t nb = 0, nr = 0;
+			rc = vc_block_loop(rd, k, block_bases, [&](const char *q, size_t l) {
+				if (seq_out && nb + l <= seq_cap) memcpy(seq_out + nb, q, l);
+				if (lens_out && nr < lens_cap) lens_out[nr] = (uint32_t)l;
+				nb += l;
+				++nr;
+				return VC_OK;
+			}, local);
+		}
 		local.seconds = mono_now() - t0;
 		*st = local;
 		return rc;

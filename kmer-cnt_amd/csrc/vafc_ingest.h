@@ -1,9 +1,10 @@
-// vafc_ingest.h -- parallel ingest of a plain (uncompressed) FASTA/FASTQ file
-// with the reference's exact semantics.
+// vafc_ingest.h -- parallel ingest of a FASTA/FASTQ text with the
+// reference's exact semantics: a plain file read
+// with pread, or a gzip file's text as the parallel inflater produces it.
 //
 // The reference reads a file with one kseq stream inside kt_pipeline step 0
-// (vaf-counter.c:486-517, kseq.h:192-232).  Here the file is cut into pieces
-// that worker threads parse concurrently with pread:
+// (vaf-counter.c:486-517, kseq.h:192-232).  Here the text is cut into pieces
+// that worker threads parse concurrently:
 //
 //   * piece j covers the nominal byte range [j P, (j+1) P).  Its worker guesses
 //     the first record header at or after j P (the FASTQ four-line shape, or
@@ -29,6 +30,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "vafc.h"
 #include "vafc_fastq.h"
@@ -82,10 +84,41 @@ public:
 	virtual int submit(int slot, const VcSlotBuf &b, uint64_t n, uint64_t bytes) = 0;
 };
 
-// Whole-file pass over an open plain file of `size` bytes.  threads >= 1
-// parse workers, `slots` >= threads + 1 slot buffers owned by the sink,
-// pieces of `piece_bytes`.  Fills st (bases, seqs, blocks; not seconds).
+// The text the pieces are cut from.
+class VcIngestSource : public VcTextSource {
+public:
+	// Whether the text is longer than off bytes (waits until that is known).
+	virtual bool longer_than(uint64_t off) = 0;
+	// No byte before off will be read again.
+	virtual void release(uint64_t) {}
+	// The pass ended early: wake and end every read (short reads from now on).
+	virtual void abort() {}
+};
+
+// Whole-text pass.  threads >= 1 parse workers, `slots` >= threads + 1 slot
+// buffers owned by the sink (piece j uses slot j % slots), pieces of
+// `piece_bytes`.  Fills st (bases, seqs, blocks; not seconds).
+int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int slots, uint64_t piece_bytes,
+                   VcIngestSink &sink, vc_file_stats &st);
+
+// An open plain file of `size` bytes.
 int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, int slots,
                     uint64_t piece_bytes, VcIngestSink &sink, vc_file_stats &st);
+
+// A gzip file opened with vc_gzp_open (vafc_gzip.h; the caller closes it): a
+// pump thread copies the inflated stream into a window of blocks that the
+// parse workers read (at most about `window_bytes` buffered ahead of the
+// oldest piece still needed, unless a worker waits for more).
+class VcGzParallel;
+// Parse workers for gzip input inflated by `threads` workers: the inflate
+// is several times slower per byte than the parse ($VAFC_GZ_PARSERS overrides).
+inline int vc_gz_parse_threads(int threads)
+{
+	const char *e = getenv("VAFC_GZ_PARSERS");
+	const int n = e && atoi(e) > 0 ? atoi(e) : (threads + 3) / 5;
+	return n < 1 ? 1 : n;
+}
+int vc_ingest_gzip(VcGzParallel *g, int k, int block_bases, int threads, int slots, uint64_t piece_bytes,
+                   uint64_t window_bytes, VcIngestSink &sink, vc_file_stats &st);
 
 #endif

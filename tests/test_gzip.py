@@ -244,3 +244,31 @@ def test_crc32_matches_zlib():
         init = int(rng.integers(0, 2 ** 32))
         got = vafc.lib().vc_gz_crc32(init, a.ctypes.data_as(ctypes.c_void_p), n)
         assert got == zlib.crc32(a.tobytes(), init), n
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_parallel_parse_of_gzip_matches_sequential(tmp_path, monkeypatch, seed):
+    """The gzip text parsed in parallel (vc_ingest_gzip: a pump thread feeding
+    parse workers, pieces down to tens of bytes, records longer than the
+    buffered window) against the sequential gzread reader, on fuzzed FASTQ /
+    FASTA with malformed records: same reads, bases, sequences and blocks."""
+    import vafc
+    from test_reader import _fuzz_file
+    rng = np.random.default_rng(300 + seed)
+    src = str(tmp_path / "f.fq")
+    _fuzz_file(src, rng, 1500)
+    raw = open(src, "rb").read()
+    if seed == 3:   # long FASTA records, far beyond the window of tiny pieces
+        raw = b"".join(b">s%d\n%s\n" % (i, np.frombuffer(b"ACGTN", np.uint8)[rng.integers(0, 5, n)].tobytes())
+                       for i, n in enumerate([50, 120_000, 7, 300_000, 90]))
+    p = str(tmp_path / "f.fq.gz")
+    with open(p, "wb") as f:
+        f.write(_member(raw, level=1 + seed))
+    for piece, parsers in ((37 + 50 * seed, 3), (1 << 20, 2), (4096, 1)):
+        monkeypatch.setenv("VAFC_INGEST_PIECE", str(piece))
+        monkeypatch.setenv("VAFC_GZ_PARSERS", str(parsers))
+        for k, b in ((9, 10_000_000), (5, 60)):
+            st0, r0 = vafc.scan_file(p, k, b, with_reads=True)
+            st1, r1 = vafc.scan_file_parallel(p, k, b, threads=4, piece_bytes=2048, with_reads=True)
+            assert (st1.bases, st1.seqs, st1.blocks) == (st0.bases, st0.seqs, st0.blocks), (piece, k, b)
+            assert r1 == r0
