@@ -211,7 +211,8 @@ def main():
                          "c3 (k=31, 100M pairs = 200M reads of 150 bp), c4 (1B reads in total split over "
                          "the GPUs: strong scaling), c5 (200k-SNP synthetic panel)")
     ap.add_argument("--cpu-reads", type=int, default=2_000_000, help="CPU baseline sample")
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline timings (the parity sample still runs)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the live parity sample too")
     ap.add_argument("--e2e-reads", type=int, default=16_000_000, help="reads of the end-to-end FASTQ")
     ap.add_argument("--no-e2e", action="store_true")
     args = ap.parse_args()
@@ -347,7 +348,7 @@ def main():
     cpu = None
     parity = None
     e2e = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_parity:
         n = min(args.cpu_reads, R)
         kind = "reference" if os.path.exists(REF_CLI) else "port"
         binary = REF_CLI if kind == "reference" else PORT_CLI
@@ -355,17 +356,20 @@ def main():
             fq = os.path.join(tmp, "sample.fq")
             write_fastq_from_device(d_seq, n, L, fq)
             # -t 1, -t 4, -t <CPU share> and -t nproc, median of
-            # 3 each; the best median is the baseline
+            # 3 each; the best median is the baseline (--no-cpu: one -t 1 run,
+            # for parity only)
             runs = {}
-            for t in sorted({1, 4, cpu_share(), os.cpu_count() or 1}):
+            for t in (sorted({1, 4, cpu_share(), os.cpu_count() or 1}) if not args.no_cpu else []):
                 rs = []
                 for rep in range(3):
                     r = cli_run(binary, pat, fq, t, os.path.join(tmp, "ref_t%d.vaf" % t), args.k, timeout=600)
                     rs.append(r)
                     log("cpu %s -t %d (run %d): %.2f Mbases/s (%.1fs)" % (kind, t, rep + 1, r["mbases"], r["wall"]))
                 runs[t] = sorted(rs, key=lambda r: r["mbases"])[1]
-            best_t = max(runs, key=lambda t: runs[t]["mbases"])
-            cpu = {"value": runs[best_t]["mbases"], "unit": "Mbases/sec",
+            if args.no_cpu:
+                cli_run(binary, pat, fq, 1, os.path.join(tmp, "ref_t1.vaf"), args.k, timeout=600)
+            best_t = max(runs, key=lambda t: runs[t]["mbases"]) if runs else None
+            cpu = None if not runs else {"value": runs[best_t]["mbases"], "unit": "Mbases/sec",
                    "cores": 2 + best_t if best_t > 1 else 3,
                    "kind": kind,
                    "threads_flag": best_t, "host_cpus": os.cpu_count(), "cpu_share": cpu_share(),

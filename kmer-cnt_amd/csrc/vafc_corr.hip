@@ -253,12 +253,11 @@ extern "C" int vc_vafset_snps(const vc_vafset *s, int i)
 
 // One .vaf file; *truncated = the 100,000-row cap was hit (the caller prints
 // the reference's warning).  false if the file cannot be opened.
-static bool vaf_load_one(const char *path, std::string &nm, std::vector<double> &x, std::vector<int32_t> &d,
-                         bool &truncated)
+// load_vaf_file's body on an opened file (closed here)
+static void vaf_load_fp(FILE *fp, const char *path, std::string &nm, std::vector<double> &x,
+                        std::vector<int32_t> &d, bool &truncated)
 {
 	truncated = false;
-	FILE *fp = fopen(path, "r");
-	if (!fp) return false;
 	// sample name: basename, at most 255 bytes, cut at the first ".vaf"
 	const char *base = strrchr(path, '/');
 	nm.assign(base ? base + 1 : path);
@@ -282,6 +281,14 @@ static bool vaf_load_one(const char *path, std::string &nm, std::vector<double> 
 		d.push_back(tot);
 	}
 	fclose(fp);
+}
+
+static bool vaf_load_one(const char *path, std::string &nm, std::vector<double> &x, std::vector<int32_t> &d,
+                         bool &truncated)
+{
+	FILE *fp = fopen(path, "r");
+	if (!fp) return false;
+	vaf_load_fp(fp, path, nm, x, d, truncated);
 	return true;
 }
 
@@ -303,31 +310,41 @@ extern "C" int vc_vafset_add(vc_vafset *s, const char *path)
 extern "C" int vc_vafset_add_many(vc_vafset *s, const char *const *paths, int n, int n_threads, int *n_added,
                                   uint8_t *truncated)
 {
-	if (!s || n < 0 || (n && (!paths || !n_added || !truncated))) return VC_EINVAL;
+	if (!s || n < 0 || (n && (!paths || !truncated))) return VC_EINVAL;
 	std::vector<std::string> nm(n);
 	std::vector<std::vector<double>> x(n);
 	std::vector<std::vector<int32_t>> d(n);
-	std::vector<char> ok(n, 0), tr(n, 0);
+	std::vector<char> tr(n, 0);
+	// the files are opened here, in order, up to the first that cannot be
+	// opened, as the reference's loop does (nothing after it is opened: a
+	// FIFO named after a missing file must not block); workers read them
+	std::vector<FILE *> fp;
+	for (int i = 0; i < n; ++i) {
+		FILE *f = fopen(paths[i], "r");
+		if (!f) break;
+		fp.push_back(f);
+	}
+	const int m = (int)fp.size();
 	std::atomic<int> next(0);
 	const int T = n_threads < 1 ? 1 : (n_threads > 64 ? 64 : n_threads);
 	std::vector<std::thread> th;
-	for (int t = 0; t < T && t < n; ++t)
+	for (int t = 0; t < T && t < m; ++t)
 		th.emplace_back([&] {
-			for (int i; (i = next.fetch_add(1)) < n;) {
+			for (int i; (i = next.fetch_add(1)) < m;) {
 				bool trunc = false;
-				ok[i] = vaf_load_one(paths[i], nm[i], x[i], d[i], trunc);
+				vaf_load_fp(fp[(size_t)i], paths[i], nm[i], x[i], d[i], trunc);
 				tr[i] = trunc;
 			}
 		});
 	for (auto &t : th) t.join();
 	int i = 0;
-	for (; i < n && ok[i]; ++i) {                  // in order, up to the first file that failed
+	for (; i < m; ++i) {                           // in order, up to the first file that failed
 		truncated[i] = (uint8_t)tr[i];
 		s->name.push_back(std::move(nm[i]));
 		s->x.push_back(std::move(x[i]));
 		s->d.push_back(std::move(d[i]));
 	}
-	*n_added = i;
+	if (n_added) *n_added = i;
 	return i == n ? VC_OK : VC_EIO;
 }
 

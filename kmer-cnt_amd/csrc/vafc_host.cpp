@@ -254,6 +254,7 @@ struct vc_ctx {
 	uint32_t *own_counts = nullptr;
 	unsigned long long *own_tally = nullptr;
 	uint32_t *d_nlong = nullptr;
+	uint32_t *d_flags = nullptr;           // kernel error flags (VcKernelArgs::flags)
 	uint8_t *d_pad = nullptr;              // 64 B staging for inputs under 16 B (kernels load 16 B)
 	uint32_t *d_long = nullptr;
 	uint32_t long_cap = 0;
@@ -387,6 +388,8 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	c->d_counts = c->own_counts;
 	c->d_tally = c->own_tally;
 	TRY(hipMalloc(&c->d_nlong, sizeof(uint32_t)));
+	TRY(hipMalloc(&c->d_flags, sizeof(uint32_t)));
+	TRY(hipMemset(c->d_flags, 0, sizeof(uint32_t)));
 	TRY(hipMalloc(&c->d_pad, 64));
 	TRY(hipMemset(c->d_pad, 0, 64));
 	TRY(hipMemcpy(c->d_table, tab.data(), tslots * sizeof(vc_slot_t), hipMemcpyHostToDevice));
@@ -453,6 +456,7 @@ extern "C" void vc_destroy(vc_ctx *c)
 	if (c->own_counts) (void)hipFree(c->own_counts);
 	if (c->own_tally) (void)hipFree(c->own_tally);
 	if (c->d_nlong) (void)hipFree(c->d_nlong);
+	if (c->d_flags) (void)hipFree(c->d_flags);
 	if (c->d_pad) (void)hipFree(c->d_pad);
 	if (c->d_long) (void)hipFree(c->d_long);
 	if (c->kc) {
@@ -521,6 +525,7 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 {
 	if (n_reads == 0) return VC_OK;
 	if (c->kc) return kc_launch(c, d_seq, seq_bytes, d_offs, d_lens, n_reads, st);
+	if (n_reads > 0xFFFFFFFFull) return VC_EINVAL;   // the long-read list holds u32 read indices
 	int rc = ensure_long_cap(c, seq_bytes);
 	if (rc != VC_OK) return rc;
 	VcKernelArgs A;
@@ -555,6 +560,7 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 	A.nlong = c->d_nlong;
 	A.longlist = c->d_long;
 	A.long_cap = c->long_cap;
+	A.flags = c->d_flags;
 	uint64_t groups = (n_reads + VC_BLOCK - 1) / VC_BLOCK;
 	int grid = (int)(groups < (uint64_t)c->n_cu ? groups : (uint64_t)c->n_cu);
 	HIPCK(hipMemsetAsync(c->d_nlong, 0, sizeof(uint32_t), st));
@@ -658,6 +664,19 @@ static int reduce_shards(vc_ctx *c);
 extern "C" int vc_finish(vc_ctx *c, uint32_t *counts, uint64_t *kmers)
 {
 	if (!c) return VC_EINVAL;
+	if (!c->kc)
+		for (int i = 0; i < n_shards(c); ++i) {   // kernel error flags (a sync point anyway)
+			vc_ctx *sh = shard_at(c, i);
+			uint32_t f = 0;
+			HIPCK(hipSetDevice(sh->dev));
+			HIPCK(hipStreamSynchronize(sh->st));
+			HIPCK(hipMemcpy(&f, sh->d_flags, sizeof f, hipMemcpyDeviceToHost));
+			if (f & 1u) {
+				fprintf(stderr, "[E::vafc] more reads longer than %d bases than the long-read list holds "
+				        "(overlapping device reads?): counts incomplete\n", VC_LONG_READ);
+				return VC_EINVAL;
+			}
+		}
 	if (!c->rep.empty()) {
 		int rc = reduce_shards(c);
 		if (rc != VC_OK) return rc;
@@ -700,6 +719,7 @@ extern "C" int vc_reset(vc_ctx *c)
 	}
 	HIPCK(hipMemsetAsync(c->d_counts, 0, 2 * (size_t)c->n_patterns * sizeof(uint32_t), c->st));
 	HIPCK(hipMemsetAsync(c->d_tally, 0, sizeof(unsigned long long), c->st));
+	HIPCK(hipMemsetAsync(c->d_flags, 0, sizeof(uint32_t), c->st));
 	for (vc_ctx *r : c->rep) {
 		int rc = vc_reset(r);
 		if (rc != VC_OK) return rc;

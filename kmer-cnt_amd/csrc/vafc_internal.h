@@ -36,6 +36,7 @@ struct VcKernelArgs {
 	uint32_t *nlong;             // long-read list fill (zeroed per launch)
 	uint32_t *longlist;
 	uint32_t long_cap;
+	uint32_t *flags;             // bit 0: more long reads than long_cap (sticky until vc_reset)
 };
 
 // LDS: prefilter words + 4 zero words (16-byte aligned), then the per-wave queues.

@@ -814,6 +814,7 @@ vc_count_long_kernel(VcKernelArgs A)
 {
 	const uint32_t nl_raw = *A.nlong;
 	const uint32_t nl = nl_raw < A.long_cap ? nl_raw : A.long_cap;
+	if (nl_raw > A.long_cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(A.flags, 1u);   // reported by vc_finish
 	if (nl == 0) return;   // uniform over the grid
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 	uint32_t *filt = smem;

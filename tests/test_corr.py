@@ -202,7 +202,20 @@ def test_loader_parallel_matches_sequential(work, threads):
         C_.load_vaf_files(fns[:3] + ["/nonexistent/x.vaf"] + fns[3:], threads)
     assert e.value.code == vafc.VC_EIO and len(C_) == 3
     assert [C_.name(i) for i in range(3)] == ["other", "big", "messy"]
-    for S in (A, B, C_):
+    # nothing after the first unopenable file is opened: a FIFO there (no
+    # writer) would block the call forever if it were
+    fifo = os.path.join(work, "after_missing_%d.fifo" % threads)
+    if not os.path.exists(fifo):
+        os.mkfifo(fifo)
+    D = vafc.VafSamples()
+    with pytest.raises(vafc.VafcError):
+        D.load_vaf_files(fns[:2] + ["/nonexistent/x.vaf", fifo] + fns[2:], threads)
+    assert len(D) == 2
+    # n_added may be NULL
+    arr = (vafc.C.c_char_p * 1)(fns[0].encode())
+    assert vafc.lib().vc_vafset_add_many(D._h, vafc.C.cast(arr, vafc.P), 1, threads, None,
+                                         np.zeros(1, np.uint8).ctypes.data_as(vafc.P)) == 0
+    for S in (A, B, C_, D):
         S.close()
 
 

@@ -340,8 +340,16 @@ def test_large_panel_c5_shape():
     assert int(got.sum()) > 20_000
 
 
-def test_full_size_linearity_and_prefix_parity(torch_dev):
-    """At BASELINE size (100M reads, HBM-resident): count(all) == count(first half) +
+FULL_SIZE = {   # BASELINE.json configs at their full size on one GPU
+    "c2": (21, "grch38", 100_000_000),    # 100M reads, ~20k SNPs
+    "c3": (31, "grch38", 200_000_000),    # 100M pairs = 200M reads, k = 31
+    "c5": (21, "syn200k", 100_000_000),   # 200k-SNP panel, 100M reads
+}
+
+
+@pytest.mark.parametrize("config", sorted(FULL_SIZE))
+def test_full_size_linearity_and_prefix_parity(torch_dev, config):
+    """At BASELINE size (HBM-resident): count(all) == count(first half) +
     count(second half) (mod 2^32), k-mer tallies add up, and an exact 1M-read prefix
     matches the oracle."""
     import torch
@@ -349,8 +357,9 @@ def test_full_size_linearity_and_prefix_parity(torch_dev):
     import vafc_synth as S
     import oracle as O
     import tempfile
-    panel = S.grch38_panel()
-    R, L = 100_000_000, 150
+    k, panel_name, R = FULL_SIZE[config]
+    panel = S.grch38_panel() if panel_name == "grch38" else S.make_panel(S.synthetic_bed(200_000))
+    L = 150
     d_seq = torch.empty(R * L, dtype=torch.uint8, device=torch_dev)
     d_offs = torch.empty(R, dtype=torch.int64, device=torch_dev)
     d_lens = torch.empty(R, dtype=torch.int32, device=torch_dev)
@@ -362,11 +371,11 @@ def test_full_size_linearity_and_prefix_parity(torch_dev):
     torch.cuda.synchronize()
     with tempfile.TemporaryDirectory() as d:
         pat = os.path.join(d, "p.txt")
-        panel.write_patterns(pat, 21)
+        panel.write_patterns(pat, k)
         db = vafc.load_patterns(pat)
-        keys, vals, _ = db.keys(21)
-        orc = O.Oracle(21, pattern_fn=pat)
-    m = vafc.KmerMap(21, keys, vals, db.n, 0)
+        keys, vals, _ = db.keys(k)
+        orc = O.Oracle(k, pattern_fn=pat)
+    m = vafc.KmerMap(k, keys, vals, db.n, 0)
 
     def run(first, n):
         m.reset()
@@ -382,7 +391,8 @@ def test_full_size_linearity_and_prefix_parity(torch_dev):
     b_c, b_k = m.finish()
     assert all_k == a_k + b_k
     assert np.array_equal(all_c, (a_c.astype(np.uint64) + b_c).astype(np.uint32))
-    assert all_k > R * 120
+    assert all_k > R * (150 - k - 10)
+    assert int(all_c.astype(np.uint64).sum()) > R // 200
     n = 1_000_000
     p_c, p_k = run(0, n)
     seq = d_seq[: n * L].cpu().numpy()
@@ -421,4 +431,31 @@ def test_empty_inputs():
     m.count_block(np.frombuffer(b"ACGTN" * 10, np.uint8), np.array([0, 10], np.uint64), np.array([5, 20], np.uint32))
     c, km = m.finish()
     assert int(c.sum()) == 0 and km == 0
+    m.close()
+
+
+def test_long_read_list_overflow_is_reported(torch_dev):
+    """Device reads may overlap: more reads longer than 16,384 bases than the
+    long-read list holds (sized from seq_bytes) must fail loudly in finish(),
+    never under-count silently; reset() clears the error."""
+    import torch
+    import vafc
+    rng = np.random.default_rng(8)
+    L = 20_000
+    seq = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, L)]
+    keys, vals, n_pat = table_from_reads(21, [seq.tobytes()], rng, n_pat=50)
+    m = vafc.KmerMap(21, keys, vals, n_pat, 0)
+    d_seq = torch.from_numpy(seq.copy()).to(torch_dev)
+    n = 6    # six reads on the same bytes; the list holds 20000 // 16385 + 1 = 2
+    d_offs = torch.zeros(n, dtype=torch.int64, device=torch_dev)
+    d_lens = torch.full((n,), L, dtype=torch.int32, device=torch_dev)
+    torch.cuda.synchronize()
+    m.count_device(d_seq.data_ptr(), L, d_offs.data_ptr(), d_lens.data_ptr(), n)
+    with pytest.raises(vafc.VafcError):
+        m.finish()
+    m.reset()
+    m.count_device(d_seq.data_ptr(), L, d_offs.data_ptr(), d_lens.data_ptr(), 1)
+    c, km = m.finish()
+    want, km_want = oracle_counts(21, keys, vals, n_pat, [seq.tobytes()])
+    assert km == km_want and np.array_equal(c, want)
     m.close()
