@@ -24,6 +24,8 @@ def pytest_configure(config):
 @pytest.fixture(scope="session", autouse=True)
 def built():
     """Build the oracle and the product once per session (no-op when up to date)."""
+    if os.environ.get("VAFC_SKIP_BUILD") == "1":   # sanitizer runs (tools/asan_tests.sh) bring their own build
+        return
     jobs = str(min(8, os.cpu_count() or 2))
     subprocess.run(["make", "-s", "-j", jobs, "-C", os.path.join(ROOT, "oracle")], check=True)
     subprocess.run(["make", "-s", "-j", jobs, "-C", os.path.join(PKG, "csrc")], check=True)
