@@ -94,3 +94,17 @@ def test_vaf_writer_u32_wraparound(tmp_path):
     assert f[5:8] == [str(0xFFFFFFF0), str(0x20), str((0xFFFFFFF0 + 0x20) & 0xFFFFFFFF)]
     assert float(f[8]) == pytest.approx(0x20 / 0x10, abs=1e-4)
     assert lines[0] == "# Average depth: %.2f" % ((0xFFFFFFF0 + 0x20) / db.n)
+
+
+def test_reference_binding_patch_applies():
+    """oracle/bind_reference.py finds each of its anchors exactly once in the
+    reference's vaf-counter.c (skipped where the reference is absent)."""
+    import importlib.util
+    src = "/root/reference/vaf-counter.c"
+    if not os.path.exists(src):
+        pytest.skip("reference sources not present")
+    spec = importlib.util.spec_from_file_location("bind_reference", os.path.join(ROOT, "oracle", "bind_reference.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    out = m.patch(open(src).read())
+    assert out.count("vc_count_file(") == 1 and out.count("vc_create(") == 1 and "count_fastq_kmers(argv[i]" not in out

@@ -459,3 +459,26 @@ def test_long_read_list_overflow_is_reported(torch_dev):
     want, km_want = oracle_counts(21, keys, vals, n_pat, [seq.tobytes()])
     assert km == km_want and np.array_equal(c, want)
     m.close()
+
+
+# --------------------------------------------------------------------------
+# the reference's own main() bound to libvafc.so
+# --------------------------------------------------------------------------
+
+BIND_CLI = os.path.join(os.path.dirname(PRODUCT_CLI), "..", "..", "oracle", "_ref", "vaf-counter-vafc")
+
+
+@pytest.mark.parametrize("name", CASE_NAMES)
+def test_reference_main_bound_to_libvafc(name, manifest, synth_dir, tmp_path):
+    """oracle/_ref/vaf-counter-vafc is /root/reference/vaf-counter.c patched
+    exactly as INTEGRATION.md §2 shows (oracle/bind_reference.py): its loader,
+    map and writer, with count_fastq_kmers replaced by vc_count_file.  Every
+    golden case gives the reference's .vaf, -v tallies and exit code."""
+    assert os.path.exists(BIND_CLI), "oracle/_ref/vaf-counter-vafc not built (make -C oracle)"
+    entry = next(c for c in manifest["cases"] if c["name"] == name)
+    rc, stats, data, err = run_cli(BIND_CLI, entry, synth_dir, tmp_path)
+    assert rc == entry["exit"], err[-2000:]
+    if entry["vaf_md5"] is not None:
+        assert hashlib.md5(data).hexdigest() == entry["vaf_md5"]
+        for key in ("bases", "seqs", "kmers"):
+            assert stats.get(key) == entry["stats"].get(key), key
