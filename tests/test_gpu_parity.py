@@ -446,7 +446,7 @@ def test_long_read_list_overflow_is_reported(torch_dev):
     keys, vals, n_pat = table_from_reads(21, [seq.tobytes()], rng, n_pat=50)
     m = vafc.KmerMap(21, keys, vals, n_pat, 0)
     d_seq = torch.from_numpy(seq.copy()).to(torch_dev)
-    n = 6    # six reads on the same bytes; the list holds 20000 // 16385 + 1 = 2
+    n = 70_000   # reads on the same bytes; the list holds max(2^30 // 16385 + 1, seq_bytes // 16385 + 1) = 65,537
     d_offs = torch.zeros(n, dtype=torch.int64, device=torch_dev)
     d_lens = torch.full((n,), L, dtype=torch.int32, device=torch_dev)
     torch.cuda.synchronize()
