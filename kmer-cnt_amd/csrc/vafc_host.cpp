@@ -242,6 +242,7 @@ struct vc_ctx {
 	int n_cu = 256;
 	vc_slot_t *d_table = nullptr;
 	int ablate = 0;                   // kernel ablation variant (libvafc_abl.so only)
+	uint32_t variant = 0;             // kernel A/B experiment knobs ($VAFC_VARIANT, tools/ab.py)
 	int nt4 = 0;                      // seq_nt4 decode everywhere (vc_set_nt4_decode)
 	uint32_t tbits = 0;
 	uint32_t *d_filter = nullptr;
@@ -360,7 +361,11 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 		tab[s].val = vals[i];
 		const uint32_t flo = (uint32_t)key, rlo = (uint32_t)vc_revcomp(key, k);
 		fw[vc_filter_word(flo, rlo, fsh, wbits)] |= vc_filter_mask(flo, rlo);
-		if (l2bits) l2w[vc_hash(key) >> (32 - l2bits)] |= vc_l2f_mask(vc_hash2(key));
+		if (l2bits) {
+			uint32_t w, b;
+			vc_l2f_mix(flo, rlo, &w, &b);
+			l2w[w >> (32 - l2bits)] |= vc_l2f_mask(b >> 17);
+		}
 		++inserted;
 	}
 	c->n_keys = inserted;
@@ -369,6 +374,7 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	c->l2bits = l2bits;
 	c->fsh = fsh;
 	c->ablate = getenv("VAFC_ABLATE") ? atoi(getenv("VAFC_ABLATE")) : 0;
+	c->variant = getenv("VAFC_VARIANT") ? (uint32_t)atoi(getenv("VAFC_VARIANT")) : 0u;
 
 	int rc = VC_OK;
 #define TRY(call)                                                                        \
@@ -552,6 +558,7 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 	A.l2f = c->d_l2f;
 	A.l2bits = c->l2bits;
 	A.ablate = c->ablate;
+	A.variant = c->variant;
 	A.nt4 = (uint32_t)c->nt4;
 	A.k = c->k;
 	A.kmask = ((uint64_t)1 << (2 * c->k)) - 1;

@@ -28,6 +28,7 @@ struct VcKernelArgs {
 	const uint32_t *l2f;         // second-level filter (vc_l2f_*), NULL = off
 	uint32_t l2bits;
 	int ablate;                  // ablation builds only (VAFC_ABLATE), 0 otherwise
+	uint32_t variant;            // A/B experiment knobs (VAFC_VARIANT), 0 = the default kernel
 	uint32_t nt4;                // 1: seq_nt4_table decode everywhere (snp-pattern-gen), 0: vaf-counter
 	int k;
 	uint64_t kmask;              // (1 << 2k) - 1
