@@ -62,14 +62,14 @@ def log(msg):
     sys.stderr.flush()
 
 
-def cpu_share():
-    """Host threads this process may use: the affinity mask, at most 16 (the
-    GPU box's CPU share per GPU; os.cpu_count() there is the whole machine)."""
+def cpu_share(gpus=1):
+    """Host threads this process may use: the affinity mask, at most 16 per GPU
+    (the GPU box's CPU share; os.cpu_count() there is the whole machine)."""
     try:
         n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         n = os.cpu_count() or 1
-    return max(1, min(16, n))
+    return max(1, min(16 * gpus, n))
 
 
 def cli_run(binary, pat, fq, threads, out, k, env=None, timeout=900):
@@ -138,10 +138,13 @@ def gzip_level1(src, dst, threads, chunk=16 << 20):
     return os.path.getsize(dst)
 
 
-def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu):
+def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None):
     """The drop-in CLI end to end on a page-cached FASTQ (plain, gzip), median of
-    3 runs each, and the reference once on the plain file for .vaf parity."""
-    t = cpu_share()
+    3 runs each, and the reference once on the plain file for .vaf parity.
+    devices: several GPUs in the one CLI process (VAFC_DEVICES, vc_create_multi:
+    batches dealt round robin, one RCCL reduce); parity is then checked against
+    the single-device CLI on the same file."""
+    t = cpu_share(len(devices) if devices else 1)
     fq = os.path.join(tmp, "e2e.fq")
     gz = fq + ".gz"
     t0 = time.time()
@@ -161,6 +164,12 @@ def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu):
     env = dict(os.environ)
     env.pop("VAFC_DEVICES", None)
     env["VAFC_DEVICE"] = os.environ.get("LOCAL_RANK", "0")
+    if devices:
+        env["VAFC_DEVICES"] = ",".join(str(d) for d in devices)
+        out["devices"] = list(devices)
+        out["multi_gpu"] = ("one CLI process over %d GPUs: the parallel reader's pieces dealt round robin to "
+                            "one shard per GPU, one RCCL reduce of the counts before the .vaf is written"
+                            % len(devices))
     vafs = {}
     for name, path in (("plain", fq), ("gzip", gz)):
         runs = []
@@ -182,7 +191,14 @@ def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu):
     if cpu:
         out["plain"]["vs_cpu_baseline"] = round(out["plain"]["value"] / cpu["value"], 1)
         out["gzip"]["vs_cpu_baseline"] = round(out["gzip"]["value"] / cpu["value"], 1)
-    if os.path.exists(REF_CLI):
+    if devices:   # the single-device CLI on the same file
+        o = os.path.join(tmp, "e2e_1gpu.vaf")
+        env1 = dict(env)
+        env1.pop("VAFC_DEVICES", None)
+        r = cli_run(PRODUCT_CLI, pat, fq, cpu_share(), o, k, env=env1)
+        out["single_gpu_same_file"] = {"value": r["mbases"], "unit": "Mbases/sec", "threads": cpu_share()}
+        out["parity_vs_single_gpu"] = vafs["plain"] == md5(o) and vafs["gzip"] == vafs["plain"]
+    elif os.path.exists(REF_CLI):
         o = os.path.join(tmp, "e2e_ref.vaf")
         r = cli_run(REF_CLI, pat, fq, 1, o, k)
         log("e2e reference -t 1 on the plain file: %.1f Mbases/s (%.1fs)" % (r["mbases"], r["wall"]))
@@ -392,11 +408,17 @@ def main():
             parity = md5(gpu_vaf) == md5(os.path.join(tmp, "ref_t1.vaf"))
         except Exception as e:  # the baseline must never hide the measured line
             log("cpu baseline failed: %r" % (e,))
-    if rank == 0 and world == 1 and not args.no_e2e and args.config == "c2":
+    if rank == 0 and not args.no_e2e and args.config == "c2":
+        # N > 1: the same leg with one CLI process over all N GPUs (the other
+        # ranks wait at the barrier below)
         try:
-            e2e = e2e_leg(d_seq, L, args.k, pat, tmp, min(args.e2e_reads, R), cpu)
+            e2e = e2e_leg(d_seq, L, args.k, pat, tmp, min(args.e2e_reads, R), cpu,
+                          devices=[r % max(torch.cuda.device_count(), 1) for r in range(world)] if world > 1
+                          else None)
         except Exception as e:
             log("e2e leg failed: %r" % (e,))
+    if world > 1:
+        dist.barrier()
 
     if rank == 0:
         line = {
