@@ -99,7 +99,10 @@ struct BitIn {
 // Huffman decoding tables.  Entry: bits 0-7 code length to consume, 8-12 extra
 // bits (or sub-table index bits), 13-15 kind, 16-31 value.
 // ---------------------------------------------------------------------------
-enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_SUB = 3, K_BAD = 4 };
+// K_LIT2: two literals in one literal/length table entry (value = first |
+// second << 8, length = both codes): DNA literals have 2-3-bit codes, so most
+// 11-bit lookups of FASTQ sequence text decode a pair.
+enum : uint32_t { K_LIT = 0, K_LIT2 = 1, K_LEN = 2, K_EOB = 3, K_SUB = 4, K_BAD = 5 };
 inline uint32_t mk(uint32_t len, uint32_t ext, uint32_t kind, uint32_t val)
 {
 	return len | ext << 8 | kind << 13 | val << 16;
@@ -214,6 +217,25 @@ bool build(uint32_t *T, unsigned root, const uint8_t *lens, unsigned n, Code c)
 	return true;
 }
 
+// Literal/length root table: entries whose code leaves room for a second
+// literal code within the root bits become K_LIT2 pairs.  The next code's
+// entry is looked up on the bits after the first code (the higher root bits
+// are unknown, so it must fit in the known ones).
+void pair_literals(uint32_t *T, unsigned root)
+{
+	static thread_local uint32_t single[1u << LROOT];
+	memcpy(single, T, ((size_t)1 << root) * sizeof(uint32_t));
+	for (unsigned i = 0; i < (1u << root); ++i) {
+		const uint32_t e = single[i];
+		if (e_kind(e) != K_LIT) continue;
+		const unsigned l1 = e_len(e);
+		if (l1 >= root) continue;
+		const uint32_t e2 = single[i >> l1];
+		if (e_kind(e2) != K_LIT || e_len(e2) > root - l1) continue;
+		T[i] = mk(l1 + e_len(e2), 0, K_LIT2, e_val(e) | e_val(e2) << 8);
+	}
+}
+
 struct Tables {
 	uint32_t lit[LTAB];
 	uint32_t dist[DTAB];
@@ -226,6 +248,7 @@ const Tables &fixed_tables()
 		uint8_t l[288];
 		for (int i = 0; i < 288; ++i) l[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
 		build(f->lit, LROOT, l, 288, C_LIT);
+		pair_literals(f->lit, LROOT);
 		uint8_t d[32];
 		memset(d, 5, sizeof d);
 		build(f->dist, DROOT, d, 32, C_DIST);
@@ -276,7 +299,9 @@ bool read_dynamic(BitIn &in, Tables &T)
 		i += rep;
 	}
 	if (in.overrun() || lens[256] == 0) return false;
-	return build(T.lit, LROOT, lens, hlit, C_LIT) && build(T.dist, DROOT, lens + hlit, hdist, C_DIST);
+	if (!build(T.lit, LROOT, lens, hlit, C_LIT) || !build(T.dist, DROOT, lens + hlit, hdist, C_DIST)) return false;
+	pair_literals(T.lit, LROOT);
+	return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -381,22 +406,31 @@ int decode_huff(BitIn &in, const Tables &T, Out &o)
 		uint32_t e = T.lit[in.buf & ((1u << LROOT) - 1)];
 		if (e_kind(e) == K_SUB) e = T.lit[e_val(e) + ((in.buf >> LROOT) & ((1u << e_ext(e)) - 1))];
 		in.drop(e_len(e));
-		if (e_kind(e) == K_LIT) {
+		if (e_kind(e) <= K_LIT2) {
+			// one or two literals per entry, written as a pair (the second
+			// slot of a single literal is overwritten next); up to three more
+			// root entries without a refill: >= 56 bits after it, the first
+			// code <= 15 bits, root literal entries <= 11 bits, and every
+			// lookup has >= 11 valid bits
 			size_t n = WIDE ? o.ns : o.nt;
-			if (WIDE) o.s[n++] = (uint16_t)e_val(e);
-			else o.t[n++] = (uint8_t)e_val(e);
-			// up to two more literals without a refill (56 - 15 >= 2 x 15 + 11)
-			uint32_t e2 = T.lit[in.buf & ((1u << LROOT) - 1)];
-			if (e_kind(e2) == K_LIT) {
-				in.drop(e_len(e2));
-				if (WIDE) o.s[n++] = (uint16_t)e_val(e2);
-				else o.t[n++] = (uint8_t)e_val(e2);
-				e2 = T.lit[in.buf & ((1u << LROOT) - 1)];
-				if (e_kind(e2) == K_LIT) {
-					in.drop(e_len(e2));
-					if (WIDE) o.s[n++] = (uint16_t)e_val(e2);
-					else o.t[n++] = (uint8_t)e_val(e2);
+			auto put = [&](uint32_t x) {
+				const uint32_t v = e_val(x);
+				if (WIDE) {
+					o.s[n] = (uint16_t)(v & 0xFFu);
+					o.s[n + 1] = (uint16_t)(v >> 8);
+				} else {
+					const uint16_t v16 = (uint16_t)v;
+					memcpy(o.t + n, &v16, 2);
 				}
+				n += 1u + e_kind(x);
+			};
+			put(e);
+#pragma GCC unroll 3
+			for (int x = 0; x < 3; ++x) {
+				const uint32_t e2 = T.lit[in.buf & ((1u << LROOT) - 1)];
+				if (e_kind(e2) > K_LIT2) break;
+				in.drop(e_len(e2));
+				put(e2);
 			}
 			if (WIDE) o.ns = n;
 			else o.nt = n;
@@ -461,13 +495,111 @@ int decode_huff(BitIn &in, const Tables &T, Out &o)
 	}
 }
 
+// decode_huff<false> with the bit reader and the output cursor in locals:
+// stores through the byte pointer may alias any memory, so fields of `in` and
+// `o` would otherwise be reloaded after every literal written.  Same results.
+int decode_huff_narrow(BitIn &in, const Tables &T, Out &o)
+{
+	const uint8_t *const p = in.p;
+	const uint64_t n = in.n;
+	uint64_t pos = in.pos, buf = in.buf;
+	unsigned cnt = in.cnt;
+	uint8_t *t = o.t;
+	size_t nt = o.nt, capt = o.capt;
+	const int64_t floor = o.floor;
+	const uint32_t *const LT = T.lit, *const DT = T.dist;
+	auto save = [&]() {
+		in.pos = pos;
+		in.buf = buf;
+		in.cnt = cnt;
+		o.nt = nt;
+	};
+	for (;;) {
+		if (__builtin_expect(capt - nt < 600, 0)) {
+			save();
+			if (!o.room(600)) return 0;
+			t = o.t;
+			capt = o.capt;
+		}
+		if (__builtin_expect(pos > n + 16, 0)) {
+			save();
+			return 0;
+		}
+		if (__builtin_expect(pos + 8 <= n, 1)) {   // BitIn::refill
+			uint64_t w;
+			memcpy(&w, p + pos, 8);
+			buf |= w << cnt;
+			pos += (63 - cnt) >> 3;
+			cnt |= 56;
+		} else {
+			while (cnt <= 56) {
+				const uint64_t b = pos < n ? p[pos] : 0;
+				buf |= b << cnt;
+				++pos;
+				cnt += 8;
+			}
+		}
+		uint32_t e = LT[buf & ((1u << LROOT) - 1)];
+		if (e_kind(e) == K_SUB) e = LT[e_val(e) + ((buf >> LROOT) & ((1u << e_ext(e)) - 1))];
+		buf >>= e_len(e);
+		cnt -= e_len(e);
+		if (e_kind(e) <= K_LIT2) {   // see decode_huff
+			uint16_t v16 = (uint16_t)e_val(e);
+			memcpy(t + nt, &v16, 2);
+			nt += 1u + e_kind(e);
+#pragma GCC unroll 3
+			for (int x = 0; x < 3; ++x) {
+				const uint32_t e2 = LT[buf & ((1u << LROOT) - 1)];
+				if (e_kind(e2) > K_LIT2) break;
+				buf >>= e_len(e2);
+				cnt -= e_len(e2);
+				v16 = (uint16_t)e_val(e2);
+				memcpy(t + nt, &v16, 2);
+				nt += 1u + e_kind(e2);
+			}
+			continue;
+		}
+		if (e_kind(e) == K_EOB) {
+			save();
+			return in.overrun() ? 0 : 1;
+		}
+		if (e_kind(e) != K_LEN) {
+			save();
+			return 0;
+		}
+		const unsigned lx = e_ext(e);
+		const unsigned len = e_val(e) + (unsigned)(buf & ((1ull << lx) - 1));
+		buf >>= lx;
+		cnt -= lx;
+		uint32_t d = DT[buf & ((1u << DROOT) - 1)];
+		if (e_kind(d) == K_SUB) d = DT[e_val(d) + ((buf >> DROOT) & ((1u << e_ext(d)) - 1))];
+		if (e_kind(d) == K_BAD) {
+			save();
+			return 0;
+		}
+		buf >>= e_len(d);
+		cnt -= e_len(d);
+		const unsigned dx = e_ext(d);
+		const unsigned dist = e_val(d) + (unsigned)(buf & ((1ull << dx) - 1));
+		buf >>= dx;
+		cnt -= dx;
+		// every source byte lies in t[nt - 32768, nt): literal text
+		if (__builtin_expect((int64_t)nt - (int64_t)dist < floor, 0)) {
+			save();
+			return 0;
+		}
+		copy_match8(t + nt, dist, len);
+		nt += len;
+	}
+}
+
 int decode_huff_any(BitIn &in, const Tables &T, Out &o)
 {
 	if (o.wide) {
 		const int r = decode_huff<true>(in, T, o);
 		if (r != 2) return r;
 	}
-	return decode_huff<false>(in, T, o);
+	return decode_huff_narrow(in, T, o);
 }
 
 // Stored block body; the 3 header bits are consumed.
