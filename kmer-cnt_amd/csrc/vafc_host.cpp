@@ -1227,7 +1227,8 @@ extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n
 		close(fd);
 		if (gz) {   // parallel inflate + parallel parse (falls through if the inflater declines the file)
 			const char *ce = getenv("VAFC_GZ_CHUNK");            // test knob: compressed bytes per chunk
-			VcGzParallel *g = vc_gzp_open(path, clamp_threads(n_threads), ce ? (uint64_t)atoll(ce) : 0);
+			VcGzParallel *g = vc_gzp_open(path, vc_gz_inflate_threads(clamp_threads(n_threads)),
+			                              ce ? (uint64_t)atoll(ce) : 0);
 			if (g) {
 				int rc = count_file_gzip(c, g, block_bases, n_threads, local);
 				vc_gzp_close(g);

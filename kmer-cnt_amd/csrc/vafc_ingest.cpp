@@ -605,7 +605,7 @@ extern "C" int vc_scan_file_parallel(const char *path, int k, int block_bases, i
 		// pieces of $VAFC_INGEST_PIECE (default 16 MB) -- vc_count_file's reader
 		close(fd);
 		int rc;
-		VcGzParallel *g = vc_gzp_open(path, n_threads, piece_bytes);
+		VcGzParallel *g = vc_gzp_open(path, vc_gz_inflate_threads(n_threads), piece_bytes);
 		if (g) {
 			const char *pe = getenv("VAFC_INGEST_PIECE");
 			const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : ((uint64_t)16 << 20);

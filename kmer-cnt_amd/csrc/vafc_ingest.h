@@ -118,6 +118,15 @@ inline int vc_gz_parse_threads(int threads)
 	const int n = e && atoi(e) > 0 ? atoi(e) : (threads + 3) / 5;
 	return n < 1 ? 1 : n;
 }
+// Inflate workers for gzip input: -t of them, next to the parse workers
+// (measured on a 16-CPU share: 16 inflate + 3 parse workers beat 13 + 3 and
+// 11 + 3, profiles/r02_gz_sweep3.log); $VAFC_GZ_INFLATERS overrides.
+inline int vc_gz_inflate_threads(int threads)
+{
+	const char *e = getenv("VAFC_GZ_INFLATERS");
+	if (e && atoi(e) > 0) return atoi(e);
+	return threads < 1 ? 1 : threads;
+}
 int vc_ingest_gzip(VcGzParallel *g, int k, int block_bases, int threads, int slots, uint64_t piece_bytes,
                    uint64_t window_bytes, VcIngestSink &sink, vc_file_stats &st);
 

@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--parsers", default="1,2,3,4,6")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--scaling", default="", help="also time the inflater alone at these thread counts")
+    ap.add_argument("--variants", default="", help="';'-separated groups of space-separated KEY=VAL env "
+                                                   "settings, each timed with the CLI (instead of --parsers)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -51,7 +54,13 @@ def main():
     del d_seq, d_offs, d_lens
     print("file: %d reads, %.2f GB text, %.2f GB gzip" % (R, os.path.getsize(fq) / 1e9, os.path.getsize(gz) / 1e9),
           flush=True)
-    for parsers in [int(x) for x in args.parsers.split(",")]:
+    for v in [x.strip() for x in args.variants.split(";") if x.strip()]:
+        env = dict(os.environ, **dict(kv.split("=", 1) for kv in v.split()))
+        rs = [bench.cli_run(bench.PRODUCT_CLI, pat, gz, args.threads, os.path.join(tmp, "o.vaf"), 21, env=env)
+              for _ in range(args.reps)]
+        print("%-60s CLI %s Mbases/s (process %s s)" % (v, [round(r["mbases"]) for r in rs],
+                                                        [round(r["wall"], 2) for r in rs]), flush=True)
+    for parsers in ([int(x) for x in args.parsers.split(",")] if not args.variants else []):
         env = dict(os.environ, VAFC_GZ_PARSERS=str(parsers))
         rs = [bench.cli_run(bench.PRODUCT_CLI, pat, gz, args.threads, os.path.join(tmp, "o.vaf"), 21, env=env)
               for _ in range(args.reps)]
@@ -67,6 +76,14 @@ def main():
     t0 = time.time()
     n = vafc.lib().vc_gz_inflate_parallel(gz.encode(), args.threads, 0, None, 0, None)
     print("inflate only: %.0f MB/s of text" % (n / (time.time() - t0) / 1e6), flush=True)
+    for th in [int(x) for x in args.scaling.split(",") if x]:
+        best = 1e9
+        for _ in range(2):
+            t0 = time.time()
+            n = vafc.lib().vc_gz_inflate_parallel(gz.encode(), th, 0, None, 0, None)
+            best = min(best, time.time() - t0)
+        print("inflate only, %2d threads: %.0f MB/s of text (%.0f per thread)" % (th, n / best / 1e6, n / best / 1e6 / th),
+              flush=True)
     import shutil
     shutil.rmtree(tmp, ignore_errors=True)
 
