@@ -80,51 +80,17 @@ VC_HD uint32_t vc_filter_mask(uint32_t flo, uint32_t rlo) { return (1u << (flo &
  * prefilter saturates): 2^l2bits 32-bit words in HBM, small enough to stay
  * L2/MALL-resident, three bits per key.  The queue drain checks it before
  * probing the exact table, whose random 16-byte slots would otherwise come
- * from HBM for every LDS false positive.  It is keyed like the LDS filter by
- * the two strands' low 32 bits, flo = lo32(fwd) and rlo = lo32(revcomp),
- * through a mix symmetric in them (a function of the canonical k-mer): the
- * scan queues (flo, rlo) and the drain tests a window before it rebuilds,
- * orders or hashes the k-mer.  Word: the top l2bits of w, bits: b >> 17. */
+ * from HBM for every LDS false positive.  Word from vc_hash's top bits, bits
+ * from an independent second hash of the canonical key. */
 #define VC_L2F_MIN_KEYS 65536u
 #define VC_L2F_MAX_BITS 19          /* 2 MiB */
-VC_HD void vc_l2f_mix(uint32_t flo, uint32_t rlo, uint32_t *w, uint32_t *b)
+VC_HD uint32_t vc_hash2(uint64_t key)
 {
-	const uint64_t p = (uint64_t)(flo ^ 0x9E3779B9u) * (uint64_t)(rlo ^ 0x9E3779B9u);
-	const uint32_t hi = (uint32_t)(p >> 32), lo = (uint32_t)p;
-	*w = (hi ^ lo) * 0x85EBCA77u;
-	*b = (hi + (lo ^ (lo >> 15))) * 0xC2B2AE35u;
+	return ((uint32_t)(key >> 17) ^ (uint32_t)key) * 0x9E3779B1u;
 }
 VC_HD uint32_t vc_l2f_mask(uint32_t h2)
 {
 	return (1u << (h2 & 31u)) | (1u << ((h2 >> 5) & 31u)) | (1u << ((h2 >> 10) & 31u));
-}
-
-/* Reverse complement of 16 bases packed in a word (base order reversed, codes
- * complemented). */
-VC_HD uint32_t vc_rc16(uint32_t x)
-{
-#if defined(__HIP_DEVICE_COMPILE__)
-	x = __builtin_bitreverse32(~x);
-	return ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
-#else
-	x = ~x;
-	x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);
-	x = ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);
-	x = ((x >> 8) & 0x00FF00FFu) | ((x & 0x00FF00FFu) << 8);
-	return (x >> 16) | (x << 16);
-#endif
-}
-
-/* The canonical k-mer (16 <= k <= 32) from its strands' low 32 bits: flo holds
- * forward bases k-16..k-1, rlo the complements of bases 15..0, so together
- * they hold every base. */
-VC_HD uint64_t vc_canonical_fr(uint32_t flo, uint32_t rlo, int k)
-{
-	const uint32_t lb = 2u * (uint32_t)k - 32u;
-	const uint32_t lm = lb ? (1u << lb) - 1u : 0u;
-	const uint64_t f = ((uint64_t)vc_rc16(rlo) << lb) | (flo & lm);
-	const uint64_t r = ((uint64_t)vc_rc16(flo) << lb) | (rlo & lm);
-	return f < r ? f : r;
 }
 
 /* Device key table slot: 16 bytes, one load per probe step. */

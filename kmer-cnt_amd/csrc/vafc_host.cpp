@@ -361,11 +361,7 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 		tab[s].val = vals[i];
 		const uint32_t flo = (uint32_t)key, rlo = (uint32_t)vc_revcomp(key, k);
 		fw[vc_filter_word(flo, rlo, fsh, wbits)] |= vc_filter_mask(flo, rlo);
-		if (l2bits) {
-			uint32_t w, b;
-			vc_l2f_mix(flo, rlo, &w, &b);
-			l2w[w >> (32 - l2bits)] |= vc_l2f_mask(b >> 17);
-		}
+		if (l2bits) l2w[vc_hash(key) >> (32 - l2bits)] |= vc_l2f_mask(vc_hash2(key));
 		++inserted;
 	}
 	c->n_keys = inserted;

@@ -183,50 +183,36 @@ struct WaveQueue {
 // memory latency covers the whole drain.
 // Large key sets: every entry is first checked against the second-level
 // filter (one L2-resident dword), and only survivors probe the exact table.
-// The packed scan (K >= 16) queues (rlo << 32) | flo, the strands' low 32
-// bits, in this mode: the filter is keyed by them (vc_l2f_mix), so a rejected
-// entry costs a multiply-mix and one load, and only survivors rebuild the
-// canonical k-mer (vc_canonical_fr) and hash it.  The rolling scan (k < 16)
-// queues the forward k-mer, whose strands are the whole k-mers.
-template <int K>
 __device__ __forceinline__ void drain_range_l2f(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
                                              uint32_t hi, int lane)
 {
-	uint32_t fl[4], rl[4], w[4], m[4];
+	uint64_t key[4];
+	uint32_t h[4], w[4], m[4];
 	const uint32_t l2sh = 32u - A.l2bits;
 #pragma unroll
 	for (int r = 0; r < 4; ++r) {
 		const uint32_t i = lo + (uint32_t)(r * WAVE + lane);
-		fl[r] = rl[r] = 0;
+		key[r] = VC_EMPTY_KEY;
+		h[r] = 0;
 		w[r] = 0;
 		m[r] = 1;
 		if (i < hi) {
-			const uint64_t e = q[i];
-			if constexpr (K >= 16) {
-				fl[r] = (uint32_t)e;
-				rl[r] = (uint32_t)(e >> 32);
-			} else {
-				const uint64_t f = e & A.kmask;
-				fl[r] = (uint32_t)f;
-				rl[r] = (uint32_t)revcomp_dev(f, A.k);
-			}
-			uint32_t hw, hb;
-			vc_l2f_mix(fl[r], rl[r], &hw, &hb);
-			m[r] = vc_l2f_mask(hb >> 17);
-			w[r] = A.l2f[hw >> l2sh];
+			const uint64_t f = q[i] & A.kmask;
+			const uint64_t rc = revcomp_dev(f, A.k);
+			key[r] = f < rc ? f : rc;
+			h[r] = vc_hash(key[r]);
+			m[r] = vc_l2f_mask(vc_hash2(key[r]));
+			w[r] = A.l2f[h[r] >> l2sh];
 		}
 	}
 #pragma unroll
 	for (int r = 0; r < 4; ++r) {
 		if ((w[r] & m[r]) != m[r]) continue;      // also skips empty entries (w = 0, m = 1)
-		uint64_t key;
-		if constexpr (K > 16) key = vc_canonical_fr(fl[r], rl[r], K);
-		else key = fl[r] < rl[r] ? fl[r] : rl[r];  // k <= 16: the strands are the k-mers
-		uint32_t t = vc_table_slot(vc_hash(key), A.tbits);
+		uint32_t t = vc_table_slot(h[r], A.tbits);
 		for (;;) {
 			const uint4 e = *reinterpret_cast<const uint4 *>(&A.table[t]);
 			const uint64_t k2 = ((uint64_t)e.y << 32) | e.x;
-			if (k2 == key) {
+			if (k2 == key[r]) {
 				atomicAdd(&A.counts[e.z], 1u);
 				break;
 			}
@@ -236,23 +222,12 @@ __device__ __forceinline__ void drain_range_l2f(const VcKernelArgs &A, const uin
 	}
 }
 
-// (the run-time-k scan appends inside a fully unrolled window loop; an inlined
-// second-level drain made that loop too large to unroll)
-template <int K>
-__device__ __noinline__ void drain_range_l2f_ool(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
-                                                 uint32_t hi, int lane)
-{
-	drain_range_l2f<K>(A, q, lo, hi, lane);
-}
-
-template <int K>
 __device__ __forceinline__ void drain_range(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
                                             uint32_t hi, int lane)
 {
 	__builtin_amdgcn_wave_barrier();
 	if (A.l2bits) {
-		if constexpr (K == 0) drain_range_l2f_ool<0>(A, q, lo, hi, lane);
-		else drain_range_l2f<K>(A, q, lo, hi, lane);
+		drain_range_l2f(A, q, lo, hi, lane);
 		return;
 	}
 	uint64_t key[4];
@@ -292,7 +267,6 @@ __device__ __forceinline__ void drain_range(const VcKernelArgs &A, const uint64_
 // Lanes with `hit` append `key` (bal = ballot(hit) != 0).  The queue is
 // normally drained once per read group (queue_flush); only a nearly full
 // queue is drained here, 64 entries from its top.
-template <int K>
 __device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q, uint64_t bal,
                                              bool hit, uint64_t key, int lane)
 {
@@ -301,7 +275,7 @@ __device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q
 	if (hit) Q.q[Q.n + pre] = key;
 	Q.n = __builtin_amdgcn_readfirstlane(Q.n + (uint32_t)__popcll(bal));
 	if (Q.n > VC_QCAP - WAVE) {
-		drain_range<K>(A, Q.q, Q.n - WAVE, Q.n, lane);
+		drain_range(A, Q.q, Q.n - WAVE, Q.n, lane);
 		Q.n -= WAVE;
 		// leave nothing in flight on this (rare) path, so that the compiler
 		// can keep counting the scan's prefetches across it
@@ -309,10 +283,9 @@ __device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q
 	}
 }
 
-template <int K>
 __device__ __forceinline__ void queue_flush(const VcKernelArgs &A, WaveQueue &Q, int lane)
 {
-	if (Q.n) drain_range<K>(A, Q.q, 0, Q.n, lane);
+	if (Q.n) drain_range(A, Q.q, 0, Q.n, lane);
 	Q.n = 0;
 }
 
@@ -469,7 +442,7 @@ __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t 
 				const bool hit = (fw[j] & fm[j]) == fm[j];
 				const uint64_t bal = __ballot(hit);
 				if constexpr ((ABL & 4) != 0) { asm volatile("" :: "s"(bal)); }
-				else if (bal) queue_append<K>(A, Q, bal, hit, ((uint64_t)fh[j] << 32) | fl[j], lane);
+				else if (bal) queue_append(A, Q, bal, hit, ((uint64_t)fh[j] << 32) | fl[j], lane);
 			}
 		}
 		w0 = w4; w1 = x1; w2 = x2; w3 = x3; w4 = x4;
@@ -603,18 +576,8 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 			// lowest pass first; lanes without one compute a garbage key they do not append
 			const uint32_t b = (uint32_t)__builtin_ctz(hm | 0x80000000u);   // hm < 2^16
 			const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, 2u * b);
-			uint32_t hi32;
-			if (A.l2bits) {
-				// large panels: the reverse strand's low 32 bits (window start s2
-				// bases into chunk c-2, as in the window loop) -- see drain_range_l2f
-				const uint32_t s2 = 48u - (uint32_t)K - b;
-				const bool up = s2 >= 16u;
-				hi32 = __builtin_amdgcn_alignbit(up ? Cc : Cm1, up ? Cm1 : Cm2, 2u * s2);
-				if constexpr (K == 16) hi32 = b == 0u ? Cc : hi32;   // s2 = 32: the window is chunk c
-			} else {
-				hi32 = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
-			}
-			queue_append<K>(A, Q, bal, has, ((uint64_t)hi32 << 32) | flo, lane);
+			const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
+			queue_append(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
 			hm &= hm - 1u;
 		}
 	}
@@ -831,12 +794,12 @@ vc_count_reads_kernel(VcKernelArgs A)
 		// drain at a group end only once the queue holds more than 112 entries
 		// (two per lane): each drain exposes one probe latency, so fewer, fuller
 		// drains cost less (C2: -1.6 %, C5: +-0; ABL 64 = a drain per group)
-		if constexpr ((ABL & 64) != 0) queue_flush<K>(A, Q, lane);
-		else if (Q.n > VC_QCAP - 2 * WAVE) queue_flush<K>(A, Q, lane);
+		if constexpr ((ABL & 64) != 0) queue_flush(A, Q, lane);
+		else if (Q.n > VC_QCAP - 2 * WAVE) queue_flush(A, Q, lane);
 		g = gn;
 		r = rn;
 	}
-	queue_flush<K>(A, Q, lane);
+	queue_flush(A, Q, lane);
 	const unsigned long long t = wave_sum_u64(tally);
 	if (lane == 0 && t) atomicAdd(A.tally, t);
 }
@@ -890,7 +853,7 @@ vc_count_long_kernel(VcKernelArgs A)
 			tally += tl;
 		}
 	}
-	queue_flush<K>(A, Q, lane);
+	queue_flush(A, Q, lane);
 	const unsigned long long t = wave_sum_u64(tally);
 	if (lane == 0 && t) atomicAdd(A.tally, t);
 }
