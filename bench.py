@@ -112,6 +112,11 @@ def gzip_level1(src, dst, threads, chunk=16 << 20):
     one deflate stream; CRC-32 and length trailer over the whole text."""
     import vafc
     size = os.path.getsize(src)
+    if size == 0:   # an empty member
+        with open(dst, "wb") as g:
+            g.write(b"\x1f\x8b\x08\x00\x00\x00\x00\x00\x04\x03" + zlib.compress(b"", 1)[2:-4] +
+                    struct.pack("<II", 0, 0))
+        return os.path.getsize(dst)
     with open(src, "rb") as f:
         mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
     try:

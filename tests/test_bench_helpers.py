@@ -1,0 +1,54 @@
+"""bench.py's host helpers (CPU): the pigz-style gzip writer used for the
+end-to-end leg produces one valid gzip member whose text is the input, the
+CPU-share rule, and the reference CLI's -v parsing."""
+import gzip
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def test_gzip_level1_is_one_member_with_the_input_text(tmp_path):
+    import bench
+    import vafc
+    rng = np.random.default_rng(0)
+    for size in (0, 1, 40_000, 3 * (1 << 20) + 17):
+        src = tmp_path / ("t%d.fq" % size)
+        data = np.frombuffer(b"ACGT\n@+I", np.uint8)[rng.integers(0, 8, size)].tobytes()
+        src.write_bytes(data)
+        dst = str(src) + ".gz"
+        bench.gzip_level1(str(src), dst, 3, chunk=1 << 20)
+        raw = open(dst, "rb").read()
+        assert raw[:4] == b"\x1f\x8b\x08\x00"
+        assert gzip.decompress(raw) == data
+        assert vafc.gz_inflate_zlib(dst) == data
+        if size:   # the product's parallel inflater reads it as gzread does, one member
+            got = vafc.gz_inflate_parallel(dst, threads=3, chunk_bytes=4096)
+            assert got is not None and got[0] == data and got[1]["members"] == 1
+
+
+def test_cpu_share_bounds():
+    import bench
+    n = len(os.sched_getaffinity(0))
+    assert bench.cpu_share() == max(1, min(16, n))
+    assert bench.cpu_share(8) == max(1, min(128, n))
+
+
+def test_cli_run_parses_reference_speed_line(tmp_path):
+    """cli_run on the reference binary (when built here): Speed, k-mer rate and
+    bases come from the -v report."""
+    import bench
+    import vafc_synth as S
+    if not os.path.exists(bench.REF_CLI):
+        import pytest
+        pytest.skip("reference binary not built")
+    panel = S.make_panel(S.synthetic_bed(200))
+    pat = str(tmp_path / "p.txt")
+    panel.write_patterns(pat, 21)
+    fq = str(tmp_path / "r.fq")
+    S.write_fastq(fq, panel, 2000, f_snp=0.5)
+    r = bench.cli_run(bench.REF_CLI, pat, fq, 1, str(tmp_path / "o.vaf"), 21)
+    assert r["bases"] == 2000 * 150 and r["mbases"] > 0 and r["mkmers"] > 0
