@@ -272,3 +272,26 @@ def test_parallel_parse_of_gzip_matches_sequential(tmp_path, monkeypatch, seed):
             st1, r1 = vafc.scan_file_parallel(p, k, b, threads=4, piece_bytes=2048, with_reads=True)
             assert (st1.bases, st1.seqs, st1.blocks) == (st0.bases, st0.seqs, st0.blocks), (piece, k, b)
             assert r1 == r0
+
+
+def test_parallel_parse_of_gzip_stops_early_without_reading_on(tmp_path, monkeypatch):
+    """A gzip FASTQ whose block loop ends at its third empty block (three
+    malformed records in a row, -b 1) followed by many megabytes of good reads:
+    the parallel parse stops there like the sequential reader (the pump and the
+    workers are released), with the same reads and blocks."""
+    import vafc
+    rng = np.random.default_rng(77)
+    good = _fastq_text(rng, 30)
+    bad = b"@x\nACGTACGTACGTACGTACGTACGT\n+\n" + b"I" * 30 + b"\n"   # quality longer: -2
+    bad = bad * 3
+    tail = _fastq_text(rng, 40_000)
+    p = str(tmp_path / "stop.fq.gz")
+    with open(p, "wb") as f:
+        f.write(_member(good + bad + tail, level=1))
+    for piece, parsers in ((512, 3), (1 << 16, 2)):
+        monkeypatch.setenv("VAFC_INGEST_PIECE", str(piece))
+        monkeypatch.setenv("VAFC_GZ_PARSERS", str(parsers))
+        st0, r0 = vafc.scan_file(p, 21, 1, with_reads=True)
+        st1, r1 = vafc.scan_file_parallel(p, 21, 1, threads=4, piece_bytes=4096, with_reads=True)
+        assert (st1.bases, st1.seqs, st1.blocks) == (st0.bases, st0.seqs, st0.blocks)
+        assert r1 == r0 and st0.seqs == 30
