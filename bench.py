@@ -266,6 +266,9 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        # host-side group for waiting while rank 0 runs the e2e leg on every
+        # GPU (a gloo barrier does not keep an RCCL kernel spinning on them)
+        cpu_group = dist.new_group(backend="gloo")
     import vafc
     import vafc_synth as S
 
@@ -423,7 +426,7 @@ def main():
         except Exception as e:
             log("e2e leg failed: %r" % (e,))
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=cpu_group)
 
     if rank == 0:
         line = {
