@@ -496,7 +496,7 @@ __device__ __forceinline__ int clamp16(int v) { return v < 0 ? 0 : (v > 16 ? 16 
 // One 16-base chunk c of the packed scan from its five dwords (w0: the dword
 // holding the chunk's first byte, realigned by sh); (B1, C1) / (B2, C2) are
 // the streams of chunks c-1 / c-2 and move on to c / c-1.
-template <int K, int ABL>
+template <int K, int ABL, int J0 = 0>
 __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int tail_c, int nt4m, uint32_t sh,
                                              uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
                                              uint32_t &Bm1, uint32_t &Bm2, uint32_t &Cm1, uint32_t &Cm2,
@@ -528,9 +528,10 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 	uint32_t hm = 0;                                 // filter pass, bit 15 - j for base j
 	// pass <=> bits (flo & 31) and (rlo & 31) of the filter word are set:
 	// hm = (hm << 1) | ((w >> flo) & (w >> rlo) & 1), 4 VALU per window
+	// windows j < J0 are known invalid (see scan_span_packed) and not looked up
 	uint32_t fw[16], fl[16], rl[16];
 #pragma unroll
-	for (int j = 0; j < 16; ++j) {
+	for (int j = J0; j < 16; ++j) {
 		const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, (uint32_t)(2 * (15 - j)));
 		const int s2 = j - K + 1 + 32;               // window start relative to chunk c-2
 		uint32_t rlo;
@@ -545,7 +546,7 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 		rl[j] = rlo;
 	}
 #pragma unroll
-	for (int j = 0; j < 16; ++j)
+	for (int j = J0; j < 16; ++j)
 		hm = (hm << 1) | ((fw[j] >> (fl[j] & 31u)) & (fw[j] >> (rl[j] & 31u)) & 1u);
 	// windows of this chunk inside [vlo, vhi) with no earlier invalid base
 	uint32_t V = ((1u << clamp16(U)) - 1u) & ~((1u << clamp16(Qe)) - 1u);
@@ -668,6 +669,8 @@ __device__ __forceinline__ void quad_fix(uint32_t sft, uint32_t &a, uint32_t &b,
 	}
 }
 
+template <int J> struct J0Tag { static constexpr int value = J; };
+
 // Chunks are processed in pairs.  The 8 dwords of the next pair are requested
 // (two dwordx4 from the same lines, back to back) while the current pair is
 // scanned, so each load has two chunks of work to hide behind.  The steady
@@ -719,7 +722,8 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 			it = 1;
 		}
 	}
-	for (; it + 2 < nit; it += 2) {
+	auto trip = [&](auto j0tag) {
+		constexpr int J0 = decltype(j0tag)::value;
 		const int c = c_lo + it;
 		uint32_t n0, n1, n2, n3, n4, n5, n6, n7, dn0, dn4;
 		if constexpr ((ABL & 2) != 0) {
@@ -749,13 +753,22 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 		}
 		quad_fix(d1, w1, w2, w3, w4);
 		quad_fix(d5, w5, w6, w7, w8);
-		packed_chunk<K, ABL>(A, c, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
+		packed_chunk<K, ABL, J0>(A, c, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
 		packed_chunk<K, ABL>(A, c + 1, tail_c, nt4m, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
 		w0 = w8;
 		w1 = n0; w2 = n1; w3 = n2; w4 = n3; d1 = dn0;
 		w5 = n4; w6 = n5; w7 = n6; w8 = n7; d5 = dn4;
 		wi += 8;
+	};
+	// chunk 1 of a whole read: its windows end at 16..31, those before K - 1
+	// are invalid, so its first K - 17 filter lookups are skipped
+	if constexpr (!HAS_LO && K >= 18 && (ABL & 32) == 0) {
+		if (it == 1 && it + 2 < nit) {
+			trip(J0Tag<K - 17>{});
+			it += 2;
+		}
 	}
+	for (; it + 2 < nit; it += 2) trip(J0Tag<0>{});
 	if constexpr ((ABL & 16) != 0) tl += abl_sink & 1u;
 	if (it < nit) {
 		const int c = c_lo + it;
