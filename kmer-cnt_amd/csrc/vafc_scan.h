@@ -491,6 +491,23 @@ __device__ __forceinline__ uint32_t pairrev(uint32_t x)
 	return ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
 }
 
+// The 2-bit codes of a chunk's 16 bases from its four decoded dwords, base j
+// at bits 2j.  One multiply gathers a dword's four codes (bits 0-1 of each
+// byte) into its top byte: code r times 2^(6m), m = 1..4, lands at bit
+// 8r + 6m, the top byte takes m = 4 - r, and the other products sit in
+// disjoint 2-bit fields below bit 24 (no carries).  Two v_perm_b32 and an OR
+// join the four top bytes.
+__device__ __forceinline__ uint32_t pack_codes(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3)
+{
+	const uint32_t g0 = (t0 & 0x03030303u) * 0x01041040u;
+	const uint32_t g1 = (t1 & 0x03030303u) * 0x01041040u;
+	const uint32_t g2 = (t2 & 0x03030303u) * 0x01041040u;
+	const uint32_t g3 = (t3 & 0x03030303u) * 0x01041040u;
+	const uint32_t lo = __builtin_amdgcn_perm(g1, g0, 0x0C0C0703u);   // bytes 0, 1: g0, g1 top bytes
+	const uint32_t hi = __builtin_amdgcn_perm(g3, g2, 0x07030C0Cu);   // bytes 2, 3: g2, g3 top bytes
+	return lo | hi;
+}
+
 __device__ __forceinline__ int clamp16(int v) { return v < 0 ? 0 : (v > 16 ? 16 : v); }
 
 // One 16-base chunk c of the packed scan from its five dwords (w0: the dword
@@ -518,10 +535,7 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 	}
 	U += 16;
 	Qe += 16;
-	// pack the chunk's codes: byte r of A holds bases r, 4+r, 8+r, 12+r
-	const uint32_t Am = (t0 & 0x03030303u) | ((t1 & 0x03030303u) << 2) |
-	                    ((t2 & 0x03030303u) << 4) | ((t3 & 0x03030303u) << 6);
-	const uint32_t L = transpose2x4x4(Am);          // base j at bits 2j
+	const uint32_t L = pack_codes(t0, t1, t2, t3);  // base j at bits 2j
 	const uint32_t Cc = ~L;                          // complement codes, little-endian
 	const uint32_t Bc = pairrev(L);                  // big-endian codes
 
@@ -607,9 +621,7 @@ __device__ __forceinline__ void packed_streams(int c, int tail_c, int nt4m, uint
 	}
 	U += 16;
 	Qe += 16;
-	const uint32_t Am = (t0 & 0x03030303u) | ((t1 & 0x03030303u) << 2) |
-	                    ((t2 & 0x03030303u) << 4) | ((t3 & 0x03030303u) << 6);
-	const uint32_t L = transpose2x4x4(Am);
+	const uint32_t L = pack_codes(t0, t1, t2, t3);
 	const uint32_t anyinv = (t0 | t1 | t2 | t3) & 0x04040404u;
 	if (__ballot(anyinv != 0u)) {
 		if (anyinv != 0u) {   // as in packed_chunk: U moves to the last invalid base
