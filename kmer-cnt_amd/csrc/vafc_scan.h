@@ -711,6 +711,11 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	w0 = SAFE ? s32[wi] : ldw(s32, wi, wmax);
 	uint32_t d1 = ldq_s<SAFE>(s32, wi + 1, wmax, w1, w2, w3, w4);
 	uint32_t d5 = ldq_s<SAFE>(s32, wi + 5, wmax, w5, w6, w7, w8);
+	// whole reads, K >= 17: chunk 0 only builds streams (below), so chunk 2's
+	// dwords are needed one chunk after chunk 1's and are requested up front
+	constexpr bool PEEL = !HAS_LO && K >= 17 && (ABL & 32) == 0;
+	[[maybe_unused]] uint32_t x5 = 0, x6 = 0, x7 = 0, x8 = 0, d9 = 0;
+	if constexpr (PEEL) d9 = ldq_s<SAFE>(s32, wi + 9, wmax, x5, x6, x7, x8);
 
 	uint32_t Bm1 = 0, Bm2 = 0, Cm1 = 0, Cm2 = 0;   // streams of the two previous chunks
 	int U = 1 - K - vlo + 16 * c_lo;                 // +16 at the top of every chunk
@@ -721,15 +726,17 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	// Whole reads, K >= 17: no window ends in chunk 0 (positions 0..15 < K - 1),
 	// so chunk 0 only builds the streams (about 16 % fewer VALU for 150 bp
 	// reads); the pair loop then starts at chunk 1.  The dwords of chunk 1 are
-	// w4..w8 already, chunk 2's are loaded here, and everything after moves on
-	// by 16 bytes -- the loads stay within the group's clear range (at most
-	// 8 ceil(nit / 2) + 9 dwords from the first).
-	if constexpr (!HAS_LO && K >= 17 && (ABL & 32) == 0) {
-		if (nit > 0) {
+	// w4..w8 already, chunk 2's were requested with them (x5..x8: requested
+	// here, the large-panel config waited a whole memory latency at chunk 2,
+	// +4.5 %), and everything after moves on by 16 bytes -- the loads stay
+	// within the group's clear range (8 ceil(nit / 2) + 13 dwords from the
+	// first).  A.variant bit 0 turns this off at run time (A/B).
+	if constexpr (PEEL) {
+		if (nit > 0 && (A.variant & 1u) == 0) {
 			quad_fix(d1, w1, w2, w3, w4);
 			packed_streams<K>(c_lo, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe);
 			w0 = w4; w1 = w5; w2 = w6; w3 = w7; w4 = w8; d1 = d5;
-			d5 = ldq_s<SAFE>(s32, wi + 9, wmax, w5, w6, w7, w8);
+			w5 = x5; w6 = x6; w7 = x7; w8 = x8; d5 = d9;
 			wi += 4;
 			it = 1;
 		}
@@ -775,7 +782,7 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	// chunk 1 of a whole read: its windows end at 16..31, those before K - 1
 	// are invalid, so its first K - 17 filter lookups are skipped
 	if constexpr (!HAS_LO && K >= 18 && (ABL & 32) == 0) {
-		if (it == 1 && it + 2 < nit) {
+		if (it == 1 && it + 2 < nit && (A.variant & 2u) == 0) {
 			trip(J0Tag<K - 17>{});
 			it += 2;
 		}
@@ -862,10 +869,10 @@ vc_count_reads_kernel(VcKernelArgs A)
 		const int nch = (len + 15) >> 4;
 		const int nit = wave_max_i32(nch);
 		uint32_t tl = 0;
-		// the packed scan loads dwords [off/4, off/4 + 8 ceil(nit/2) + 9) (lanes
+		// the packed scan loads dwords [off/4, off/4 + 8 ceil(nit/2) + 13) (lanes
 		// past their span keep loading); groups clear of the buffer end skip the
 		// per-load clamping
-		const bool clear = (off >> 2) + 8u * (uint64_t)((nit + 1) >> 1) + 9u <= wmax;
+		const bool clear = (off >> 2) + 8u * (uint64_t)((nit + 1) >> 1) + 13u <= wmax;
 		if (K >= 16 && __builtin_amdgcn_ballot_w64(!clear) == 0)
 			scan_any<K, false, ABL, true>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tl, lane);
 		else
