@@ -99,13 +99,10 @@ struct BitIn {
 // Huffman decoding tables.  Entry: bits 0-7 code length to consume, 8-12 extra
 // bits (or sub-table index bits), 13-15 kind, 16-31 value.
 // ---------------------------------------------------------------------------
-// The literal/length table's decoding entries are 64-bit (see pack_literals):
-// the low 32 bits are laid out as above, except that a K_LIT entry holds a
-// run of one to five literals: bits 16-18 their count, bits 24-63 the bytes
-// (first in the lowest byte), bits 0-7 the length of all their codes.  DNA
-// literals have 2-3-bit codes, so an 11-bit lookup of FASTQ sequence text
-// decodes about four of them.
-enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_SUB = 3, K_BAD = 4 };
+// K_LIT2: two literals in one literal/length table entry (value = first |
+// second << 8, length = both codes): DNA literals have 2-3-bit codes, so most
+// 11-bit lookups of FASTQ sequence text decode a pair.
+enum : uint32_t { K_LIT = 0, K_LIT2 = 1, K_LEN = 2, K_EOB = 3, K_SUB = 4, K_BAD = 5 };
 inline uint32_t mk(uint32_t len, uint32_t ext, uint32_t kind, uint32_t val)
 {
 	return len | ext << 8 | kind << 13 | val << 16;
@@ -114,13 +111,6 @@ inline uint32_t e_len(uint32_t e) { return e & 0xff; }
 inline uint32_t e_ext(uint32_t e) { return (e >> 8) & 31; }
 inline uint32_t e_kind(uint32_t e) { return (e >> 13) & 7; }
 inline uint32_t e_val(uint32_t e) { return e >> 16; }
-inline uint32_t e_len(uint64_t e) { return (uint32_t)e & 0xff; }
-inline uint32_t e_ext(uint64_t e) { return ((uint32_t)e >> 8) & 31; }
-inline uint32_t e_kind(uint64_t e) { return ((uint32_t)e >> 13) & 7; }
-inline uint32_t e_val(uint64_t e) { return ((uint32_t)e >> 16) & 0xFFFF; }   // not for K_LIT
-inline uint32_t e_nlit(uint64_t e) { return ((uint32_t)e >> 16) & 7; }        // K_LIT: literals
-inline uint64_t e_lits(uint64_t e) { return e >> 24; }                         // K_LIT: their bytes
-constexpr unsigned MAX_LITS = 5;
 
 const uint16_t LBASE[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115,
                             131, 163, 195, 227, 258};
@@ -227,47 +217,29 @@ bool build(uint32_t *T, unsigned root, const uint8_t *lens, unsigned n, Code c)
 	return true;
 }
 
-// The 64-bit literal/length decoding table from the code's 32-bit entries S
-// (build): a root entry whose literal code leaves room in the root bits takes
-// the literals that follow it as well, up to MAX_LITS.  Each next code's entry
-// is looked up on the bits after the codes before it (the higher root bits are
-// unknown, so it must fit in the known ones).
-void pack_literals(uint64_t *T, const uint32_t *S, unsigned root, size_t total)
+// Literal/length root table: entries whose code leaves room for a second
+// literal code within the root bits become K_LIT2 pairs.  The next code's
+// entry is looked up on the bits after the first code (the higher root bits
+// are unknown, so it must fit in the known ones).
+void pair_literals(uint32_t *T, unsigned root)
 {
-	for (size_t i = 0; i < total; ++i) {
-		const uint32_t e = S[i];
-		T[i] = e_kind(e) == K_LIT ? (uint64_t)(e_len(e) | K_LIT << 13 | 1u << 16) | (uint64_t)(e_val(e) & 0xFF) << 24
-		                          : (uint64_t)e;
-	}
+	static thread_local uint32_t single[1u << LROOT];
+	memcpy(single, T, ((size_t)1 << root) * sizeof(uint32_t));
 	for (unsigned i = 0; i < (1u << root); ++i) {
-		const uint32_t e = S[i];
+		const uint32_t e = single[i];
 		if (e_kind(e) != K_LIT) continue;
-		unsigned used = e_len(e), n = 1;
-		uint64_t bytes = e_val(e) & 0xFF;
-		while (n < MAX_LITS && used < root) {
-			const uint32_t e2 = S[i >> used];
-			if (e_kind(e2) != K_LIT || e_len(e2) > root - used) break;
-			bytes |= (uint64_t)(e_val(e2) & 0xFF) << (8 * n);
-			used += e_len(e2);
-			++n;
-		}
-		T[i] = (uint64_t)(used | K_LIT << 13 | n << 16) | bytes << 24;
+		const unsigned l1 = e_len(e);
+		if (l1 >= root) continue;
+		const uint32_t e2 = single[i >> l1];
+		if (e_kind(e2) != K_LIT || e_len(e2) > root - l1) continue;
+		T[i] = mk(l1 + e_len(e2), 0, K_LIT2, e_val(e) | e_val(e2) << 8);
 	}
 }
 
 struct Tables {
-	uint64_t lit[LTAB];
+	uint32_t lit[LTAB];
 	uint32_t dist[DTAB];
 };
-
-// The literal/length code's decoding table (build + pack_literals).
-bool build_lit(uint64_t *T, const uint8_t *lens, unsigned n)
-{
-	static thread_local uint32_t tmp[LTAB];
-	if (!build(tmp, LROOT, lens, n, C_LIT)) return false;
-	pack_literals(T, tmp, LROOT, LTAB);
-	return true;
-}
 
 const Tables &fixed_tables()
 {
@@ -275,7 +247,8 @@ const Tables &fixed_tables()
 		Tables *f = new Tables;
 		uint8_t l[288];
 		for (int i = 0; i < 288; ++i) l[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
-		build_lit(f->lit, l, 288);
+		build(f->lit, LROOT, l, 288, C_LIT);
+		pair_literals(f->lit, LROOT);
 		uint8_t d[32];
 		memset(d, 5, sizeof d);
 		build(f->dist, DROOT, d, 32, C_DIST);
@@ -326,7 +299,9 @@ bool read_dynamic(BitIn &in, Tables &T)
 		i += rep;
 	}
 	if (in.overrun() || lens[256] == 0) return false;
-	return build_lit(T.lit, lens, hlit) && build(T.dist, DROOT, lens + hlit, hdist, C_DIST);
+	if (!build(T.lit, LROOT, lens, hlit, C_LIT) || !build(T.dist, DROOT, lens + hlit, hdist, C_DIST)) return false;
+	pair_literals(T.lit, LROOT);
+	return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -413,164 +388,116 @@ inline void copy_match8(uint8_t *dst, unsigned dist, unsigned len)
 	}
 }
 
-// Eight literals widened to phase-1 symbols in one 16-byte store (the ones
-// past a run are overwritten next; the output keeps 600 slots of room).
-inline void put_wide(uint16_t *d, uint64_t v)
+// One Huffman-coded block body up to its end-of-block code.  Returns 1 at
+// the end of the block, 0 on an error, 2 (phase 1 only) when the output has
+// just switched to phase 2 and the block continues there.
+template <bool WIDE>
+int decode_huff(BitIn &in, const Tables &T, Out &o)
 {
-	_mm_storeu_si128((__m128i *)d, _mm_unpacklo_epi8(_mm_cvtsi64_si128((long long)v), _mm_setzero_si128()));
-}
-
-// One Huffman-coded block body up to its end-of-block code, in phase 1
-// (16-bit symbols; see Out).  Returns 1 at the end of the block, 0 on an
-// error, 2 when the output has just switched to phase 2 and the block
-// continues there (decode_huff_narrow).  The bit reader, the output cursor
-// and the marker state live in locals: stores through the symbol pointer
-// would otherwise make the compiler reload them after every write.
-int decode_huff_wide(BitIn &in, const Tables &T, Out &o)
-{
-	const uint8_t *const p = in.p;
-	const uint64_t n = in.n;
-	uint64_t pos = in.pos, buf = in.buf;
-	unsigned cnt = in.cnt;
-	uint16_t *s = o.s;
-	size_t ns = o.ns, caps = o.caps;
-	int64_t last_mark = o.last_mark;
-	uint32_t min_mark = o.min_mark;
-	const int64_t floor = o.floor;
-	const uint64_t *const LT = T.lit;
-	const uint32_t *const DT = T.dist;
-	auto save = [&]() {
-		in.pos = pos;
-		in.buf = buf;
-		in.cnt = cnt;
-		o.ns = ns;
-		o.last_mark = last_mark;
-		o.min_mark = min_mark;
-	};
 	for (;;) {
-		if (__builtin_expect((int64_t)ns - last_mark > (int64_t)WSIZE, 0)) {
-			save();
-			return o.narrow() ? 2 : 0;
-		}
-		if (__builtin_expect(caps - ns < 600, 0)) {
-			save();
-			if (!o.room(600)) return 0;
-			s = o.s;
-			caps = o.caps;
-		}
-		if (__builtin_expect(pos > n + 16, 0)) {
-			save();
-			return 0;
-		}
-		if (__builtin_expect(pos + 8 <= n, 1)) {   // BitIn::refill
-			uint64_t w;
-			memcpy(&w, p + pos, 8);
-			buf |= w << cnt;
-			pos += (63 - cnt) >> 3;
-			cnt |= 56;
+		if (WIDE) {
+			if (__builtin_expect((int64_t)o.ns - o.last_mark > (int64_t)WSIZE, 0)) return o.narrow() ? 2 : 0;
+			if (__builtin_expect(o.caps - o.ns < 600, 0) && !o.room(600)) return 0;
 		} else {
-			while (cnt <= 56) {
-				const uint64_t by = pos < n ? p[pos] : 0;
-				buf |= by << cnt;
-				++pos;
-				cnt += 8;
-			}
+			if (__builtin_expect(o.capt - o.nt < 600, 0) && !o.room(600)) return 0;
 		}
-		uint64_t e = LT[buf & ((1u << LROOT) - 1)];
-		if (e_kind(e) == K_SUB) e = LT[e_val(e) + ((buf >> LROOT) & ((1u << e_ext(e)) - 1))];
-		buf >>= e_len(e);
-		cnt -= e_len(e);
-		if (e_kind(e) == K_LIT) {
-			// a run of literals per entry; up to three more root entries
-			// without a refill: >= 56 bits after it, the first code <= 15
-			// bits, root literal entries <= 11 bits, and every lookup has
-			// >= 11 valid bits
-			put_wide(s + ns, e_lits(e));
-			ns += e_nlit(e);
+		if (__builtin_expect(in.pos > in.n + 16, 0)) return 0;
+		in.refill();
+		uint32_t e = T.lit[in.buf & ((1u << LROOT) - 1)];
+		if (e_kind(e) == K_SUB) e = T.lit[e_val(e) + ((in.buf >> LROOT) & ((1u << e_ext(e)) - 1))];
+		in.drop(e_len(e));
+		if (e_kind(e) <= K_LIT2) {
+			// one or two literals per entry, written as a pair (the second
+			// slot of a single literal is overwritten next); up to three more
+			// root entries without a refill: >= 56 bits after it, the first
+			// code <= 15 bits, root literal entries <= 11 bits, and every
+			// lookup has >= 11 valid bits
+			size_t n = WIDE ? o.ns : o.nt;
+			auto put = [&](uint32_t x) {
+				const uint32_t v = e_val(x);
+				if (WIDE) {
+					o.s[n] = (uint16_t)(v & 0xFFu);
+					o.s[n + 1] = (uint16_t)(v >> 8);
+				} else {
+					const uint16_t v16 = (uint16_t)v;
+					memcpy(o.t + n, &v16, 2);
+				}
+				n += 1u + e_kind(x);
+			};
+			put(e);
 #pragma GCC unroll 3
 			for (int x = 0; x < 3; ++x) {
-				const uint64_t e2 = LT[buf & ((1u << LROOT) - 1)];
-				if (e_kind(e2) != K_LIT) break;
-				buf >>= e_len(e2);
-				cnt -= e_len(e2);
-				put_wide(s + ns, e_lits(e2));
-				ns += e_nlit(e2);
+				const uint32_t e2 = T.lit[in.buf & ((1u << LROOT) - 1)];
+				if (e_kind(e2) > K_LIT2) break;
+				in.drop(e_len(e2));
+				put(e2);
 			}
+			if (WIDE) o.ns = n;
+			else o.nt = n;
 			continue;
 		}
-		if (e_kind(e) == K_EOB) {
-			save();
-			return in.overrun() ? 0 : 1;
+		if (e_kind(e) == K_EOB) return in.overrun() ? 0 : 1;
+		if (e_kind(e) != K_LEN) return 0;
+		const unsigned len = e_val(e) + in.take(e_ext(e));
+		uint32_t d = T.dist[in.buf & ((1u << DROOT) - 1)];
+		if (e_kind(d) == K_SUB) d = T.dist[e_val(d) + ((in.buf >> DROOT) & ((1u << e_ext(d)) - 1))];
+		if (e_kind(d) == K_BAD) return 0;
+		in.drop(e_len(d));
+		const unsigned dist = e_val(d) + in.take(e_ext(d));
+		if (!WIDE) {   // every source byte lies in t[nt - 32768, nt): literal text
+			if ((int64_t)o.nt - (int64_t)dist < o.floor) return 0;
+			copy_match8(o.t + o.nt, dist, len);
+			o.nt += len;
+			continue;
 		}
-		if (e_kind(e) != K_LEN) {
-			save();
-			return 0;
-		}
-		const unsigned lx = e_ext(e);
-		const unsigned len = e_val(e) + (unsigned)(buf & ((1ull << lx) - 1));
-		buf >>= lx;
-		cnt -= lx;
-		uint32_t d = DT[buf & ((1u << DROOT) - 1)];
-		if (e_kind(d) == K_SUB) d = DT[e_val(d) + ((buf >> DROOT) & ((1u << e_ext(d)) - 1))];
-		if (e_kind(d) == K_BAD) {
-			save();
-			return 0;
-		}
-		buf >>= e_len(d);
-		cnt -= e_len(d);
-		const unsigned dx = e_ext(d);
-		const unsigned dist = e_val(d) + (unsigned)(buf & ((1ull << dx) - 1));
-		buf >>= dx;
-		cnt -= dx;
-		const int64_t src = (int64_t)ns - (int64_t)dist;
-		uint16_t *dst = s + ns;
+		const int64_t src = (int64_t)o.ns - (int64_t)dist;
+		uint16_t *dst = o.s + o.ns;
 		if (src >= 0) {
-			const uint16_t *sp = dst - dist;
-			if (src <= last_mark) {   // the source may hold markers: copy and look
+			const uint16_t *s = dst - dist;
+			if (src <= o.last_mark) {   // the source may hold markers: copy and look
+				uint64_t acc = 0;
 				if (dist >= 8) {   // (the look may see up to 7 symbols past the source: harmless)
-					__m128i acc = _mm_setzero_si128();
 					for (unsigned i = 0; i < len; i += 8) {
-						const __m128i v = _mm_loadu_si128((const __m128i *)(sp + i));
-						_mm_storeu_si128((__m128i *)(dst + i), v);
-						acc = _mm_or_si128(acc, v);
+						uint64_t a, b;
+						memcpy(&a, s + i, 8);
+						memcpy(&b, s + i + 4, 8);
+						memcpy(dst + i, &a, 8);
+						memcpy(dst + i + 4, &b, 8);
+						acc |= a | b;
 					}
-					if (_mm_movemask_epi8(acc) & 0xAAAA) last_mark = (int64_t)ns + len - 1;
 				} else {
-					uint16_t acc = 0;
 					for (unsigned i = 0; i < len; ++i) {
-						const uint16_t v = sp[i];
+						const uint16_t v = s[i];
 						dst[i] = v;
 						acc |= v;
 					}
-					if (acc & 0x8000u) last_mark = (int64_t)ns + len - 1;
 				}
+				if (acc & 0x8000800080008000ull) o.last_mark = (int64_t)o.ns + len - 1;
 			} else if (dist >= 8) {
-				for (unsigned i = 0; i < len; i += 8) memcpy(dst + i, sp + i, 16);
+				for (unsigned i = 0; i < len; i += 8) memcpy(dst + i, s + i, 16);
 			} else if (dist == 1) {
-				const uint16_t v = sp[0];
+				const uint16_t v = s[0];
 				for (unsigned i = 0; i < len; ++i) dst[i] = v;
 			} else {
-				for (unsigned i = 0; i < len; ++i) dst[i] = sp[i];
+				for (unsigned i = 0; i < len; ++i) dst[i] = s[i];
 			}
 		} else {
-			if (src < floor) {   // before the member's first byte
-				save();
-				return 0;
-			}
+			if (src < o.floor) return 0;   // before the member's first byte
 			const uint32_t m = (uint32_t)(src + WSIZE);
-			if (m < min_mark) min_mark = m;
+			if (m < o.min_mark) o.min_mark = m;
 			for (unsigned i = 0; i < len; ++i) {
 				const int64_t si = src + (int64_t)i;
-				dst[i] = si < 0 ? (uint16_t)(MARK | (uint32_t)(si + WSIZE)) : s[si];
+				dst[i] = si < 0 ? (uint16_t)(MARK | (uint32_t)(si + WSIZE)) : o.s[si];
 			}
-			last_mark = (int64_t)ns + len - 1;
+			o.last_mark = (int64_t)o.ns + len - 1;
 		}
-		ns += len;
+		o.ns += len;
 	}
 }
 
-// Phase 2 (byte output) of a block body, as decode_huff_wide with bytes: no
-// markers can be reached any more, back-references copy literal text.
+// decode_huff<false> with the bit reader and the output cursor in locals:
+// stores through the byte pointer may alias any memory, so fields of `in` and
+// `o` would otherwise be reloaded after every literal written.  Same results.
 int decode_huff_narrow(BitIn &in, const Tables &T, Out &o)
 {
 	const uint8_t *const p = in.p;
@@ -580,8 +507,7 @@ int decode_huff_narrow(BitIn &in, const Tables &T, Out &o)
 	uint8_t *t = o.t;
 	size_t nt = o.nt, capt = o.capt;
 	const int64_t floor = o.floor;
-	const uint64_t *const LT = T.lit;
-	const uint32_t *const DT = T.dist;
+	const uint32_t *const LT = T.lit, *const DT = T.dist;
 	auto save = [&]() {
 		in.pos = pos;
 		in.buf = buf;
@@ -613,23 +539,23 @@ int decode_huff_narrow(BitIn &in, const Tables &T, Out &o)
 				cnt += 8;
 			}
 		}
-		uint64_t e = LT[buf & ((1u << LROOT) - 1)];
+		uint32_t e = LT[buf & ((1u << LROOT) - 1)];
 		if (e_kind(e) == K_SUB) e = LT[e_val(e) + ((buf >> LROOT) & ((1u << e_ext(e)) - 1))];
 		buf >>= e_len(e);
 		cnt -= e_len(e);
-		if (e_kind(e) == K_LIT) {   // see decode_huff_wide
-			uint64_t v = e_lits(e);
-			memcpy(t + nt, &v, 8);
-			nt += e_nlit(e);
+		if (e_kind(e) <= K_LIT2) {   // see decode_huff
+			uint16_t v16 = (uint16_t)e_val(e);
+			memcpy(t + nt, &v16, 2);
+			nt += 1u + e_kind(e);
 #pragma GCC unroll 3
 			for (int x = 0; x < 3; ++x) {
-				const uint64_t e2 = LT[buf & ((1u << LROOT) - 1)];
-				if (e_kind(e2) != K_LIT) break;
+				const uint32_t e2 = LT[buf & ((1u << LROOT) - 1)];
+				if (e_kind(e2) > K_LIT2) break;
 				buf >>= e_len(e2);
 				cnt -= e_len(e2);
-				v = e_lits(e2);
-				memcpy(t + nt, &v, 8);
-				nt += e_nlit(e2);
+				v16 = (uint16_t)e_val(e2);
+				memcpy(t + nt, &v16, 2);
+				nt += 1u + e_kind(e2);
 			}
 			continue;
 		}
@@ -670,7 +596,7 @@ int decode_huff_narrow(BitIn &in, const Tables &T, Out &o)
 int decode_huff_any(BitIn &in, const Tables &T, Out &o)
 {
 	if (o.wide) {
-		const int r = decode_huff_wide(in, T, o);
+		const int r = decode_huff<true>(in, T, o);
 		if (r != 2) return r;
 	}
 	return decode_huff_narrow(in, T, o);
