@@ -312,6 +312,19 @@ bool read_dynamic(BitIn &in, Tables &T)
 // by output position, its first `res` bytes are filled in later by resolving
 // s[0..res) against the window, the rest are final when written.
 // ---------------------------------------------------------------------------
+// Large output buffers are backed by transparent huge pages where the kernel
+// allows it (THP "madvise" mode): a chunk writes tens of MB into freshly
+// grown buffers, and 4 KiB first-touch faults from many workers at once cost
+// more than the decoding (VAFC_GZ_NOHUGE=1 turns this off, A/B).
+const bool gz_huge = getenv("VAFC_GZ_NOHUGE") == nullptr;
+void advise_huge(void *p, size_t n)
+{
+	if (!gz_huge) return;
+	const uintptr_t H = (uintptr_t)2 << 20;
+	const uintptr_t a = ((uintptr_t)p + H - 1) & ~(H - 1), b = ((uintptr_t)p + n) & ~(H - 1);
+	if (b > a) madvise((void *)a, (size_t)(b - a), MADV_HUGEPAGE);
+}
+
 struct Out {
 	uint16_t *s = nullptr;             // phase 1 symbols
 	size_t ns = 0, caps = 0;
@@ -343,6 +356,7 @@ struct Out {
 		while (nc < need) nc *= 2;
 		void *q = realloc(*p, nc * elem);
 		if (!q) return false;
+		advise_huge(q, nc * elem);
 		*p = q;
 		*cap = nc;
 		return true;
@@ -858,12 +872,14 @@ struct Piece {
 	std::vector<uint32_t> seg_crc;    // events.size() + 1 segments
 	bool stream_end = false;
 	bool ready = false, resolving = false;
+	int lent = 0;                     // spans handed out with a hold (vc_gzp_span_hold), not yet released
 	~Piece() { free(text); }
 	bool reserve(size_t c)
 	{
 		if (c <= cap) return true;
 		uint8_t *q = (uint8_t *)realloc(text, c);
 		if (!q) return false;
+		advise_huge(q, c);
 		text = q;
 		cap = c;
 		return true;
@@ -1023,7 +1039,8 @@ public:
 	~VcGzParallel() { shutdown(); }
 	bool start(const char *path, int threads, uint64_t chunk_bytes);
 	int64_t read(uint8_t *dst, size_t n);
-	int64_t span(const uint8_t **out, size_t maxn);
+	int64_t span(const uint8_t **out, size_t maxn, void **hold = nullptr);
+	void release(void *hold);
 	void get_stats(VcGzStats *st)
 	{
 		std::lock_guard<std::mutex> lk(mu_);
@@ -1044,6 +1061,7 @@ private:
 	uint64_t next_decode_ = 0;
 	std::deque<std::unique_ptr<Piece>> pieces_;
 	std::vector<std::unique_ptr<Piece>> spare_;
+	std::vector<std::unique_ptr<Piece>> lent_;    // read, but spans of them still held
 	size_t max_pieces_ = 8;
 	std::vector<std::thread> workers_;
 	std::thread seq_;
@@ -1364,9 +1382,11 @@ bool VcGzParallel::start(const char *path, int threads, uint64_t chunk_bytes)
 	if (nchunks_ == 0) nchunks_ = 1;
 	stats.chunks = nchunks_;
 	if (threads < 1) threads = 1;
-	slots_.resize((size_t)threads + 2);
+	size_t extra = 2;
+	if (const char *e = getenv("VAFC_GZ_SLOTS")) extra = (size_t)atoi(e);   // A/B knob: slots beyond the workers
+	slots_.resize((size_t)threads + extra);
 	for (auto &s : slots_) s.reset(new Chunk);
-	max_pieces_ = (size_t)threads + 4;
+	max_pieces_ = (size_t)threads + extra + 2;
 	fixed_tables();
 	for (int t = 0; t < threads; ++t) workers_.emplace_back(&VcGzParallel::worker, this);
 	seq_ = std::thread(&VcGzParallel::sequencer, this);
@@ -1375,7 +1395,7 @@ bool VcGzParallel::start(const char *path, int threads, uint64_t chunk_bytes)
 
 // The next bytes of the stream without a copy: *out points into the current
 // piece, valid until the next call (the piece is released then).
-int64_t VcGzParallel::span(const uint8_t **out, size_t maxn)
+int64_t VcGzParallel::span(const uint8_t **out, size_t maxn, void **hold)
 {
 	for (;;) {
 		if (done_ || maxn == 0) return 0;
@@ -1383,8 +1403,10 @@ int64_t VcGzParallel::span(const uint8_t **out, size_t maxn)
 			const bool last = cur_->stream_end;
 			{
 				std::lock_guard<std::mutex> lk(mu_);
-				spare_.push_back(std::move(pieces_.front()));
+				std::unique_ptr<Piece> P = std::move(pieces_.front());
 				pieces_.pop_front();
+				if (P->lent > 0) lent_.push_back(std::move(P));   // back once every hold is released
+				else spare_.push_back(std::move(P));
 				cv_.notify_all();
 			}
 			cur_ = nullptr;
@@ -1409,6 +1431,11 @@ int64_t VcGzParallel::span(const uint8_t **out, size_t maxn)
 		if (rd_ < lim) {
 			const size_t take = std::min(maxn, lim - rd_);
 			*out = P.text + rd_;
+			if (hold) {
+				std::lock_guard<std::mutex> lk(mu_);
+				++P.lent;
+				*hold = &P;
+			}
 			rd_ += take;
 			stats.out_bytes += take;
 			return (int64_t)take;
@@ -1448,6 +1475,21 @@ int64_t VcGzParallel::read(uint8_t *dst, size_t n)
 	return (int64_t)got;
 }
 
+void VcGzParallel::release(void *hold)
+{
+	std::lock_guard<std::mutex> lk(mu_);
+	Piece *P = static_cast<Piece *>(hold);
+	if (--P->lent > 0) return;
+	for (size_t i = 0; i < lent_.size(); ++i)
+		if (lent_[i].get() == P) {   // already read: reusable now
+			spare_.push_back(std::move(lent_[i]));
+			lent_.erase(lent_.begin() + (long)i);
+			cv_.notify_all();
+			return;
+		}
+	// still the piece being read: it goes back when it is spent
+}
+
 void VcGzParallel::shutdown()
 {
 	if (getenv("VAFC_GZ_PROFILE"))
@@ -1481,6 +1523,10 @@ int64_t vc_gzp_read(VcGzParallel *g, uint8_t *dst, size_t n) { return g->read(ds
 
 int64_t vc_gzp_span(VcGzParallel *g, const uint8_t **p, size_t max) { return g->span(p, max); }
 
+int64_t vc_gzp_span_hold(VcGzParallel *g, const uint8_t **p, size_t max, void **hold) { return g->span(p, max, hold); }
+
+void vc_gzp_release(VcGzParallel *g, void *hold) { g->release(hold); }
+
 void vc_gzp_stats(VcGzParallel *g, VcGzStats *st) { g->get_stats(st); }
 
 void vc_gzp_close(VcGzParallel *g) { delete g; }
@@ -1495,11 +1541,11 @@ extern "C" int64_t vc_gz_inflate_parallel(const char *path, int threads, uint64_
 	VcGzParallel *g = vc_gzp_open(path, threads, chunk_bytes);
 	if (!g) return -1;
 	uint64_t tot = 0;
-	std::vector<uint8_t> tmp((size_t)1 << 20);
-	for (;;) {
-		const int64_t r = g->read(tmp.data(), tmp.size());
+	for (;;) {   // spans: no copy unless the caller wants the bytes
+		const uint8_t *q;
+		const int64_t r = g->span(&q, (size_t)1 << 20);
 		if (r <= 0) break;
-		if (out && tot < cap) memcpy(out + tot, tmp.data(), (size_t)std::min<uint64_t>((uint64_t)r, cap - tot));
+		if (out && tot < cap) memcpy(out + tot, q, (size_t)std::min<uint64_t>((uint64_t)r, cap - tot));
 		tot += (uint64_t)r;
 	}
 	if (stats6) {

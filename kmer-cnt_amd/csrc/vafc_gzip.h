@@ -54,6 +54,11 @@ int64_t vc_gzp_read(VcGzParallel *g, uint8_t *dst, size_t n);
 // The same without a copy: up to `max` next bytes at *p, valid until the next
 // call on g.
 int64_t vc_gzp_span(VcGzParallel *g, const uint8_t **p, size_t max);
+// The same, but the bytes stay valid until vc_gzp_release(g, *hold) (any
+// thread), so the caller can keep them without copying; the decoder reuses a
+// piece's buffer only once every hold on it is released.
+int64_t vc_gzp_span_hold(VcGzParallel *g, const uint8_t **p, size_t max, void **hold);
+void vc_gzp_release(VcGzParallel *g, void *hold);
 void vc_gzp_stats(VcGzParallel *g, VcGzStats *st);
 void vc_gzp_close(VcGzParallel *g);
 

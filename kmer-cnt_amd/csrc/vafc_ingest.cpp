@@ -57,9 +57,10 @@ private:
 	uint64_t size_;
 };
 
-// A gzip file's text: a pump thread takes the inflater's output in order and
-// appends it to a list of blocks; readers wait for the bytes they need.
-// Blocks wholly before the release point are freed.  The pump stays at most
+// A gzip file's text: a pump thread takes the inflater's output in order as
+// held spans (the decoder's own buffers, no copy) and appends them to a list
+// of blocks; readers wait for the bytes they need.  Blocks wholly before the
+// release point are handed back to the decoder.  The pump stays at most
 // about `window` bytes ahead of the release point unless a reader waits for
 // more (a record longer than the window must still be read).
 class GzSource : public VcIngestSource {
@@ -70,8 +71,7 @@ public:
 		abort();
 		pump_.join();
 		for (Block *b : blocks_) {
-			free(b->p);
-			delete b;
+			drop(b);
 		}
 	}
 	int64_t read(uint8_t *p, size_t n, uint64_t off) override
@@ -116,8 +116,7 @@ public:
 		if (off <= rel_) return;
 		rel_ = off;
 		while (blocks_.size() > 1 && blocks_.front()->off + blocks_.front()->len <= rel_) {
-			free(blocks_.front()->p);
-			delete blocks_.front();
+			drop(blocks_.front());
 			blocks_.pop_front();
 		}
 		room_.notify_all();
@@ -131,10 +130,11 @@ public:
 	}
 
 private:
-	struct Block {
+	struct Block {             // a span of the inflater's output, held (not copied)
 		uint64_t off = 0;      // text offset of p[0]
-		size_t len = 0, cap = 0;
-		uint8_t *p = nullptr;
+		size_t len = 0;
+		const uint8_t *p = nullptr;
+		void *hold = nullptr;  // vc_gzp_release'd once every piece before its end is parsed
 	};
 	VcGzParallel *g_;
 	uint64_t window_;
@@ -155,6 +155,13 @@ private:
 			--waiting_;
 		}
 	}
+	const bool copy_ = getenv("VAFC_GZ_COPY") != nullptr;   // A/B: copy the spans (round-2 first design)
+	void drop(Block *b)
+	{
+		if (b->hold) vc_gzp_release(g_, b->hold);
+		else free((void *)b->p);
+		delete b;
+	}
 	void pump()
 	{
 		for (;;) {
@@ -164,41 +171,28 @@ private:
 				if (aborted_) break;
 			}
 			const uint8_t *q = nullptr;
-			const int64_t n = vc_gzp_span(g_, &q, (size_t)8 << 20);
+			void *h = nullptr;
+			const int64_t n = copy_ ? vc_gzp_span(g_, &q, (size_t)8 << 20)
+			                        : vc_gzp_span_hold(g_, &q, (size_t)64 << 20, &h);
 			if (n <= 0) break;
-			// the tail block's bytes past end_ are invisible to readers, so
-			// they are written without the lock; a new block is linked under it
-			size_t done = 0;
-			while (done < (size_t)n) {
-				Block *t = nullptr;
-				{
-					std::lock_guard<std::mutex> lk(mu_);
-					t = blocks_.empty() ? nullptr : blocks_.back();
+			Block *nb = new Block;
+			if (copy_) {
+				uint8_t *c = (uint8_t *)malloc((size_t)n);
+				if (!c) {
+					delete nb;
+					break;
 				}
-				if (!t || t->len == t->cap) {
-					Block *nb = new Block;
-					nb->cap = (size_t)n - done > ((size_t)8 << 20) ? (size_t)n - done : ((size_t)8 << 20);
-					nb->p = (uint8_t *)malloc(nb->cap);
-					if (!nb->p) {
-						delete nb;
-						std::lock_guard<std::mutex> lk(mu_);
-						aborted_ = true;   // out of memory: readers see a short text
-						data_.notify_all();
-						return;
-					}
-					std::lock_guard<std::mutex> lk(mu_);
-					nb->off = end_;
-					blocks_.push_back(nb);
-					t = nb;
-				}
-				const size_t take = t->cap - t->len < (size_t)n - done ? t->cap - t->len : (size_t)n - done;
-				memcpy(t->p + t->len, q + done, take);
-				std::lock_guard<std::mutex> lk(mu_);
-				t->len += take;
-				end_ += take;
-				done += take;
-				data_.notify_all();
+				memcpy(c, q, (size_t)n);
+				q = c;
 			}
+			nb->p = q;
+			nb->len = (size_t)n;
+			nb->hold = h;
+			std::lock_guard<std::mutex> lk(mu_);
+			nb->off = end_;
+			blocks_.push_back(nb);
+			end_ += (uint64_t)n;
+			data_.notify_all();
 		}
 		std::lock_guard<std::mutex> lk(mu_);
 		eof_ = true;

@@ -4,7 +4,9 @@ reads, pigz-style gzip -1), then each libvafc.so given on the command line
 timed in its own process on vc_gz_inflate_parallel at the given thread counts
 (best of --reps), in rounds that alternate the libraries.
 
-    python tools/gz_ab.py [--reads 8000000] [--threads 1,16] LIB [LIB ...]
+    python tools/gz_ab.py [--reads 8000000] [--threads 1,16] LIB[:KEY=VAL,...] [...]
+
+(an optional `:KEY=VAL,...` suffix sets environment knobs for that variant)
 """
 import argparse
 import os
@@ -25,7 +27,7 @@ for th in %(threads)r:
         t0 = time.time()
         n = vafc.lib().vc_gz_inflate_parallel(gz.encode(), th, 0, None, 0, None)
         best = min(best, time.time() - t0)
-    print("%%s threads %%2d: %%.0f MB/s of text" %% (os.environ["VAFC_LIB"], th, n / best / 1e6), flush=True)
+    print("%%s threads %%2d: %%.0f MB/s of text" %% (os.environ["GZAB_NAME"], th, n / best / 1e6), flush=True)
 """
 
 
@@ -64,8 +66,10 @@ def main():
     print("file: %d reads, %.2f GB gzip" % (R, os.path.getsize(gz) / 1e9), flush=True)
     threads = [int(x) for x in a.threads.split(",")]
     for _ in range(a.rounds):
-        for lib in a.libs:
-            env = dict(os.environ, VAFC_LIB=os.path.abspath(lib))
+        for spec in a.libs:
+            lib, _, knobs = spec.partition(":")
+            env = dict(os.environ, VAFC_LIB=os.path.abspath(lib), GZAB_NAME=spec)
+            env.update(kv.split("=", 1) for kv in knobs.split(",") if kv)
             code = CHILD % {"root": ROOT, "gz": gz, "threads": threads, "reps": a.reps}
             subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=600)
     import shutil
