@@ -341,8 +341,10 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	// second level: >= 40 bits per key, up to 2 MiB, when the LDS filter saturates
 	uint32_t l2bits = 0;
 	if (n_keys > VC_L2F_MIN_KEYS) {
+		uint64_t bpk = 40;                                   // filter bits per key
+		if (const char *e = getenv("VAFC_L2F_BITS_PER_KEY")) bpk = strtoull(e, nullptr, 10);   // A/B knob
 		l2bits = 12;
-		while (l2bits < VC_L2F_MAX_BITS && ((uint64_t)32 << l2bits) < 40 * (uint64_t)n_keys) ++l2bits;
+		while (l2bits < VC_L2F_MAX_BITS && ((uint64_t)32 << l2bits) < bpk * (uint64_t)n_keys) ++l2bits;
 	}
 	std::vector<uint32_t> l2w(l2bits ? (size_t)1 << l2bits : 0, 0);
 	uint64_t inserted = 0;
