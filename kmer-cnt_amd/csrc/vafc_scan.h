@@ -513,7 +513,7 @@ __device__ __forceinline__ int clamp16(int v) { return v < 0 ? 0 : (v > 16 ? 16 
 // One 16-base chunk c of the packed scan from its five dwords (w0: the dword
 // holding the chunk's first byte, realigned by sh); (B1, C1) / (B2, C2) are
 // the streams of chunks c-1 / c-2 and move on to c / c-1.
-template <int K, int ABL, int J0 = 0>
+template <int K, int ABL, int J0 = 0, int J1 = 16>
 __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int tail_c, int nt4m, uint32_t sh,
                                              uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
                                              uint32_t &Bm1, uint32_t &Bm2, uint32_t &Cm1, uint32_t &Cm2,
@@ -542,10 +542,11 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 	uint32_t hm = 0;                                 // filter pass, bit 15 - j for base j
 	// pass <=> bits (flo & 31) and (rlo & 31) of the filter word are set:
 	// hm = (hm << 1) | ((w >> flo) & (w >> rlo) & 1), 4 VALU per window
-	// windows j < J0 are known invalid (see scan_span_packed) and not looked up
+	// windows j < J0 or j >= J1 are known invalid (see scan_span_packed) and
+	// not looked up
 	uint32_t fw[16], fl[16], rl[16];
 #pragma unroll
-	for (int j = J0; j < 16; ++j) {
+	for (int j = J0; j < J1; ++j) {
 		const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, (uint32_t)(2 * (15 - j)));
 		const int s2 = j - K + 1 + 32;               // window start relative to chunk c-2
 		uint32_t rlo;
@@ -560,8 +561,9 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 		rl[j] = rlo;
 	}
 #pragma unroll
-	for (int j = J0; j < 16; ++j)
+	for (int j = J0; j < J1; ++j)
 		hm = (hm << 1) | ((fw[j] >> (fl[j] & 31u)) & (fw[j] >> (rl[j] & 31u)) & 1u);
+	if constexpr (J1 < 16) hm <<= 16 - J1;          // window j at bit 15 - j
 	// windows of this chunk inside [vlo, vhi) with no earlier invalid base
 	uint32_t V = ((1u << clamp16(U)) - 1u) & ~((1u << clamp16(Qe)) - 1u);
 	const uint32_t anyinv = (t0 | t1 | t2 | t3) & 0x04040404u;
@@ -790,12 +792,23 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	for (; it + 2 < nit; it += 2) trip(J0Tag<0>{});
 	if constexpr ((ABL & 16) != 0) tl += abl_sink & 1u;
 	if (it < nit) {
-		const int c = c_lo + it;
 		quad_fix(d1, w1, w2, w3, w4);
 		quad_fix(d5, w5, w6, w7, w8);
-		packed_chunk<K, ABL>(A, c, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
-		if (it + 1 < nit)
-			packed_chunk<K, ABL>(A, c + 1, tail_c, nt4m, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl,
+		const bool pair = it + 1 < nit;
+		if (pair)
+			packed_chunk<K, ABL>(A, c_lo + it, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q,
+			                     tl, lane);
+		// the wave's last chunk: windows j end at 16 cl + j and are valid only
+		// below vhi, so when no lane has more than 8 of them (150-bp reads: 6)
+		// the upper 8 windows are not looked up (A.variant bit 2: always all)
+		const int cl = c_lo + nit - 1;
+		const uint32_t x0 = pair ? w4 : w0, x1 = pair ? w5 : w1, x2 = pair ? w6 : w2, x3 = pair ? w7 : w3,
+		               x4 = pair ? w8 : w4;
+		if ((A.variant & 4u) == 0 && __ballot(vhi - 16 * cl > 8) == 0)
+			packed_chunk<K, ABL, 0, 8>(A, cl, tail_c, nt4m, sh, x0, x1, x2, x3, x4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl,
+			                           lane);
+		else
+			packed_chunk<K, ABL>(A, cl, tail_c, nt4m, sh, x0, x1, x2, x3, x4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl,
 			                     lane);
 	}
 }
