@@ -34,6 +34,9 @@ double gz_now()
 	return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 std::atomic<uint64_t> prof_search_us{0}, prof_decode_us{0}, prof_resolve_us{0}, prof_crc_us{0};
+// waits (VAFC_GZ_PROFILE): workers idle, the sequencer waiting for the next
+// chunk / for queue room, the reader waiting for the next piece
+std::atomic<uint64_t> prof_widle_us{0}, prof_seqwait_us{0}, prof_seqpush_us{0}, prof_rdwait_us{0};
 
 constexpr uint32_t WSIZE = 32768;             // deflate history
 constexpr uint16_t MARK = 0x8000;             // symbol = MARK | window index
@@ -1104,7 +1107,9 @@ Piece *VcGzParallel::new_piece()
 bool VcGzParallel::push_piece(std::unique_ptr<Piece> P)
 {
 	std::unique_lock<std::mutex> lk(mu_);
+	const double w0 = gz_now();
 	cv_.wait(lk, [&] { return stop_ || pieces_.size() < max_pieces_; });
+	prof_seqpush_us += (uint64_t)((gz_now() - w0) * 1e6);
 	if (stop_) return false;
 	pieces_.push_back(std::move(P));
 	cv_.notify_all();
@@ -1128,6 +1133,7 @@ void VcGzParallel::worker()
 		std::unique_lock<std::mutex> lk(mu_);
 		Piece *task = nullptr;
 		Chunk *dec = nullptr;
+		const double w0 = gz_now();
 		cv_.wait(lk, [&] {
 			if (stop_) return true;
 			for (auto &P : pieces_)
@@ -1144,6 +1150,7 @@ void VcGzParallel::worker()
 			}
 			return false;
 		});
+		prof_widle_us += (uint64_t)((gz_now() - w0) * 1e6);
 		if (stop_) return;
 		if (task) {
 			task->resolving = true;
@@ -1300,7 +1307,9 @@ void VcGzParallel::sequencer()
 		Chunk *C = slots_[j % slots_.size()].get();
 		{
 			std::unique_lock<std::mutex> lk(mu_);
+			const double w0 = gz_now();
 			cv_.wait(lk, [&] { return stop_ || (C->index == j && C->decoded); });
+			prof_seqwait_us += (uint64_t)((gz_now() - w0) * 1e6);
 			if (stop_) break;
 		}
 		if (expect >= C->nom_b) {
@@ -1417,7 +1426,9 @@ int64_t VcGzParallel::span(const uint8_t **out, size_t maxn, void **hold)
 		}
 		if (!cur_) {
 			std::unique_lock<std::mutex> lk(mu_);
+			const double w0 = gz_now();
 			cv_.wait(lk, [&] { return (!pieces_.empty() && pieces_.front()->ready) || (seq_done_ && pieces_.empty()); });
+			prof_rdwait_us += (uint64_t)((gz_now() - w0) * 1e6);
 			if (pieces_.empty()) {
 				done_ = true;
 				return 0;
@@ -1493,8 +1504,11 @@ void VcGzParallel::release(void *hold)
 void VcGzParallel::shutdown()
 {
 	if (getenv("VAFC_GZ_PROFILE"))
-		fprintf(stderr, "[gzp] thread-seconds: search %.3f decode %.3f resolve %.3f crc %.3f\n", prof_search_us * 1e-6,
-		        prof_decode_us * 1e-6, prof_resolve_us * 1e-6, prof_crc_us * 1e-6);
+		fprintf(stderr,
+		        "[gzp] thread-seconds: search %.3f decode %.3f resolve %.3f crc %.3f; waits: workers %.3f "
+		        "sequencer-chunk %.3f sequencer-room %.3f reader %.3f\n",
+		        prof_search_us * 1e-6, prof_decode_us * 1e-6, prof_resolve_us * 1e-6, prof_crc_us * 1e-6,
+		        prof_widle_us * 1e-6, prof_seqwait_us * 1e-6, prof_seqpush_us * 1e-6, prof_rdwait_us * 1e-6);
 	{
 		std::lock_guard<std::mutex> lk(mu_);
 		stop_ = true;

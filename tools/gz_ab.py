@@ -7,6 +7,10 @@ timed in its own process on vc_gz_inflate_parallel at the given thread counts
     python tools/gz_ab.py [--reads 8000000] [--threads 1,16] LIB[:KEY=VAL,...] [...]
 
 (an optional `:KEY=VAL,...` suffix sets environment knobs for that variant)
+
+The first call in a fresh process runs 3-4x slower on the box than later
+ones (profiles/r02_gz_first.log; not seen on the build host), so use
+--reps >= 2 (best of) or compare like with like.
 """
 import argparse
 import os
