@@ -250,6 +250,7 @@ struct vc_ctx {
 	uint32_t *d_l2f = nullptr;             // second-level filter (large key sets only)
 	uint32_t l2bits = 0;
 	uint32_t fsh = 0;
+	uint32_t flank = 0;                    // the filter is the flank bitmap (vafc_common.h)
 	uint32_t *d_counts = nullptr;          // active outputs (own or bound)
 	unsigned long long *d_tally = nullptr;
 	uint32_t *own_counts = nullptr;
@@ -365,6 +366,30 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 		fw[vc_filter_word(flo, rlo, fsh, wbits)] |= vc_filter_mask(flo, rlo);
 		if (l2bits) l2w[vc_hash(key) >> (32 - l2bits)] |= vc_l2f_mask(vc_hash2(key));
 		++inserted;
+	}
+	// flank bitmap instead of the Bloom filter (vafc_common.h) for k >= 21 and
+	// no second level, when a random window's pass rate (about the square of
+	// the bitmap's density) stays under 1 %; VAFC_FILTER=bloom|flank forces
+	// one (A/B and tests; flank only where k allows it)
+	{
+		const char *fe = getenv("VAFC_FILTER");
+		const bool force_bloom = fe && !strcmp(fe, "bloom"), force_flank = fe && !strcmp(fe, "flank");
+		if (k >= VC_FLANK_MIN_K && !l2bits && !force_bloom) {
+			std::vector<uint32_t> fb((size_t)1 << VC_FLANK_WBITS, 0);
+			for (const vc_slot_t &e : tab)
+				if (e.key != VC_EMPTY_KEY) {
+					vc_flank_mark(fb.data(), e.key, k);
+					vc_flank_mark(fb.data(), vc_revcomp(e.key, k), k);
+				}
+			uint64_t set = 0;
+			for (uint32_t w : fb) set += (uint64_t)__builtin_popcount(w);
+			const double dens = (double)set / (double)((uint64_t)1 << (2 * VC_FLANK_BASES));
+			if (force_flank || dens <= 0.10) {
+				fw.swap(fb);
+				wbits = VC_FLANK_WBITS;
+				c->flank = 1;
+			}
+		}
 	}
 	c->n_keys = inserted;
 	c->tbits = tbits;
@@ -553,6 +578,7 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 	A.filter = c->d_filter;
 	A.wbits = c->wbits;
 	A.fsh = c->fsh;
+	A.flank = c->flank;
 	A.l2f = c->d_l2f;
 	A.l2bits = c->l2bits;
 	A.ablate = c->ablate;

@@ -11,6 +11,7 @@
 #include "vafc_common.h"
 
 #define VC_BLOCK 1024        // threads per block: 16 waves, one block per CU
+#define VC_KV_FLANK 128      // kernel variant: flank-bitmap prefilter (vc_flank_*, k >= VC_FLANK_MIN_K)
 #define VC_QCAP 240          // per-wave LDS queue entries (u64): 16 waves x 1920 B + 128 KiB filter fit in 160 KiB
 
 struct VcKernelArgs {
@@ -25,6 +26,7 @@ struct VcKernelArgs {
 	const uint32_t *filter;      // 2^wbits 32-bit words
 	uint32_t wbits;
 	uint32_t fsh;                // filter word shift (vc_filter_shift)
+	uint32_t flank;              // 1: the filter is the flank bitmap (vc_flank_*), not the Bloom filter
 	const uint32_t *l2f;         // second-level filter (vc_l2f_*), NULL = off
 	uint32_t l2bits;
 	int ablate;                  // ablation builds only (VAFC_ABLATE), 0 otherwise

@@ -510,6 +510,35 @@ __device__ __forceinline__ uint32_t pack_codes(uint32_t t0, uint32_t t1, uint32_
 
 __device__ __forceinline__ int clamp16(int v) { return v < 0 ? 0 : (v > 16 ? 16 : v); }
 
+// Flank-bitmap lookups of one chunk (VC_KV_FLANK): R with bit 15 - j set iff
+// the 10-mer ending at base j (the low 20 bits of the forward stream there) is
+// in the bitmap -- word bits 5..19, bit bits 0..4 (v_bfe_u32 uses the low 5
+// bits of its offset).  5 VALU per base: extraction, shift, mask, test, merge.
+// Bases j < J0 or j >= J1 are not looked up (their bits stay 0).
+template <int J0, int J1, int ABL = 0>
+__device__ __forceinline__ uint32_t flank_bits(uint32_t fbase, uint32_t Bm1, uint32_t Bc)
+{
+	uint32_t fw[16], fx[16];
+#pragma unroll
+	for (int j = J0; j < J1; ++j) {
+		const uint32_t x = __builtin_amdgcn_alignbit(Bm1, Bc, (uint32_t)(2 * (15 - j)));
+		const uint32_t a = x >> 3;
+		if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(a)); fw[j] = a; }
+		else fw[j] = lds_word(fbase, a, ((1u << (2 * VC_FLANK_BASES - 5)) - 1u) << 2);
+		fx[j] = x;
+	}
+	// merged with one v_lshl_or_b32 per base into two chains (the compiler's
+	// own shift + or3 tree costs 1.5 VALU per base)
+	uint32_t R0 = 0, R1 = 0;
+#pragma unroll
+	for (int j = J0; j < J1; ++j) {
+		const uint32_t t = __builtin_amdgcn_ubfe(fw[j], fx[j], 1u);
+		uint32_t &R = (j & 1) ? R1 : R0;
+		asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(R) : "v"(t), "i"(15 - j), "v"(R));
+	}
+	return R0 | R1;
+}
+
 // One 16-base chunk c of the packed scan from its five dwords (w0: the dword
 // holding the chunk's first byte, realigned by sh); (B1, C1) / (B2, C2) are
 // the streams of chunks c-1 / c-2 and move on to c / c-1.
@@ -517,8 +546,8 @@ template <int K, int ABL, int J0 = 0, int J1 = 16>
 __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int tail_c, int nt4m, uint32_t sh,
                                              uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
                                              uint32_t &Bm1, uint32_t &Bm2, uint32_t &Cm1, uint32_t &Cm2,
-                                             int &U, int &Qe, const uint32_t *__restrict__ filt, WaveQueue &Q,
-                                             uint32_t &tl, int lane)
+                                             int &U, int &Qe, uint32_t &H, const uint32_t *__restrict__ filt,
+                                             WaveQueue &Q, uint32_t &tl, int lane)
 {
 	constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
 	const uint32_t fsh = A.fsh;
@@ -540,6 +569,16 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 	const uint32_t Bc = pairrev(L);                  // big-endian codes
 
 	uint32_t hm = 0;                                 // filter pass, bit 15 - j for base j
+	if constexpr ((ABL & VC_KV_FLANK) != 0) {
+		// flank bitmap (vc_flank_*): one lookup per base, of the 10-mer ending
+		// there; window j passes iff the 10-mers ending at j (its last ten
+		// bases) and at j - (K - 10) (its first ten) are both in the set
+		(void)fsh; (void)wmask4; (void)Cm2;
+		hm = flank_bits<J0, J1, ABL>(fbase, Bm1, Bc);
+		const uint32_t P = (H << 16) | hm;           // R of chunks c-1 | c, c-2 in H >> 16
+		hm &= __builtin_amdgcn_alignbit(H >> 16, P, (uint32_t)(K - VC_FLANK_BASES));
+		H = P;
+	} else {
 	// pass <=> bits (flo & 31) and (rlo & 31) of the filter word are set:
 	// hm = (hm << 1) | ((w >> flo) & (w >> rlo) & 1), 4 VALU per window
 	// windows j < J0 or j >= J1 are known invalid (see scan_span_packed) and
@@ -564,6 +603,7 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 	for (int j = J0; j < J1; ++j)
 		hm = (hm << 1) | ((fw[j] >> (fl[j] & 31u)) & (fw[j] >> (rl[j] & 31u)) & 1u);
 	if constexpr (J1 < 16) hm <<= 16 - J1;          // window j at bit 15 - j
+	}
 	// windows of this chunk inside [vlo, vhi) with no earlier invalid base
 	uint32_t V = ((1u << clamp16(U)) - 1u) & ~((1u << clamp16(Qe)) - 1u);
 	const uint32_t anyinv = (t0 | t1 | t2 | t3) & 0x04040404u;
@@ -607,10 +647,11 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 // decode, pack, the invalid-base bookkeeping (an N here still invalidates
 // the windows that span it) and the stream rotation of packed_chunk, without
 // its 16 filter lookups, validity mask, tally or hit loop.
-template <int K>
+template <int K, int ABL>
 __device__ __forceinline__ void packed_streams(int c, int tail_c, int nt4m, uint32_t sh, uint32_t w0, uint32_t w1,
                                                uint32_t w2, uint32_t w3, uint32_t w4, uint32_t &Bm1, uint32_t &Bm2,
-                                               uint32_t &Cm1, uint32_t &Cm2, int &U, int &Qe)
+                                               uint32_t &Cm1, uint32_t &Cm2, int &U, int &Qe, uint32_t &H,
+                                               const uint32_t *__restrict__ filt)
 {
 	const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
 	const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
@@ -635,7 +676,14 @@ __device__ __forceinline__ void packed_streams(int c, int tail_c, int nt4m, uint
 			U = U < u1 ? U : u1;
 		}
 	}
-	Bm2 = Bm1; Bm1 = pairrev(L);
+	const uint32_t Bc = pairrev(L);
+	if constexpr ((ABL & VC_KV_FLANK) != 0) {
+		// the first window (ending at K - 1) starts with the 10-mer ending at
+		// base 9: chunk 0's bases 9..15 are looked up for the later windows
+		static_assert(K - VC_FLANK_BASES >= 9, "flank mode needs the first window's head in chunk 0");
+		H = flank_bits<VC_FLANK_BASES - 1, 16, ABL>(lds_base(filt), Bm1, Bc);
+	}
+	Bm2 = Bm1; Bm1 = Bc;
 	Cm2 = Cm1; Cm1 = ~L;
 }
 
@@ -720,6 +768,7 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	if constexpr (PEEL) d9 = ldq_s<SAFE>(s32, wi + 9, wmax, x5, x6, x7, x8);
 
 	uint32_t Bm1 = 0, Bm2 = 0, Cm1 = 0, Cm2 = 0;   // streams of the two previous chunks
+	uint32_t H = 0;                                  // flank mode: 10-mer hits of chunks c-2 | c-1
 	int U = 1 - K - vlo + 16 * c_lo;                 // +16 at the top of every chunk
 	int Qe = -vhi + 16 * c_lo;
 
@@ -736,7 +785,7 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	if constexpr (PEEL) {
 		if (nit > 0 && (A.variant & 1u) == 0) {
 			quad_fix(d1, w1, w2, w3, w4);
-			packed_streams<K>(c_lo, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe);
+			packed_streams<K, ABL>(c_lo, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt);
 			w0 = w4; w1 = w5; w2 = w6; w3 = w7; w4 = w8; d1 = d5;
 			w5 = x5; w6 = x6; w7 = x7; w8 = x8; d5 = d9;
 			wi += 4;
@@ -774,8 +823,8 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 		}
 		quad_fix(d1, w1, w2, w3, w4);
 		quad_fix(d5, w5, w6, w7, w8);
-		packed_chunk<K, ABL, J0>(A, c, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
-		packed_chunk<K, ABL>(A, c + 1, tail_c, nt4m, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl, lane);
+		packed_chunk<K, ABL, J0>(A, c, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q, tl, lane);
+		packed_chunk<K, ABL>(A, c + 1, tail_c, nt4m, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q, tl, lane);
 		w0 = w8;
 		w1 = n0; w2 = n1; w3 = n2; w4 = n3; d1 = dn0;
 		w5 = n4; w6 = n5; w7 = n6; w8 = n7; d5 = dn4;
@@ -783,7 +832,8 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	};
 	// chunk 1 of a whole read: its windows end at 16..31, those before K - 1
 	// are invalid, so its first K - 17 filter lookups are skipped
-	if constexpr (!HAS_LO && K >= 18 && (ABL & 32) == 0) {
+	// (flank mode looks up every base: chunk 1's are the heads of later windows)
+	if constexpr (!HAS_LO && K >= 18 && (ABL & 32) == 0 && (ABL & VC_KV_FLANK) == 0) {
 		if (it == 1 && it + 2 < nit && (A.variant & 2u) == 0) {
 			trip(J0Tag<K - 17>{});
 			it += 2;
@@ -796,7 +846,7 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 		quad_fix(d5, w5, w6, w7, w8);
 		const bool pair = it + 1 < nit;
 		if (pair)
-			packed_chunk<K, ABL>(A, c_lo + it, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q,
+			packed_chunk<K, ABL>(A, c_lo + it, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q,
 			                     tl, lane);
 		// the wave's last chunk: windows j end at 16 cl + j and are valid only
 		// below vhi, so when no lane has more than 8 of them (150-bp reads: 6)
@@ -805,10 +855,10 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 		const uint32_t x0 = pair ? w4 : w0, x1 = pair ? w5 : w1, x2 = pair ? w6 : w2, x3 = pair ? w7 : w3,
 		               x4 = pair ? w8 : w4;
 		if ((A.variant & 4u) == 0 && __ballot(vhi - 16 * cl > 8) == 0)
-			packed_chunk<K, ABL, 0, 8>(A, cl, tail_c, nt4m, sh, x0, x1, x2, x3, x4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl,
+			packed_chunk<K, ABL, 0, 8>(A, cl, tail_c, nt4m, sh, x0, x1, x2, x3, x4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q, tl,
 			                           lane);
 		else
-			packed_chunk<K, ABL>(A, cl, tail_c, nt4m, sh, x0, x1, x2, x3, x4, Bm1, Bm2, Cm1, Cm2, U, Qe, filt, Q, tl,
+			packed_chunk<K, ABL>(A, cl, tail_c, nt4m, sh, x0, x1, x2, x3, x4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q, tl,
 			                     lane);
 	}
 }
@@ -908,7 +958,7 @@ vc_count_reads_kernel(VcKernelArgs A)
 // kernel 2: long reads, every lane of the grid takes one segment
 // ---------------------------------------------------------------------------
 
-template <int K>
+template <int K, int ABL = 0>
 __global__ void __launch_bounds__(VC_BLOCK)
 vc_count_long_kernel(VcKernelArgs A)
 {
@@ -949,7 +999,7 @@ vc_count_long_kernel(VcKernelArgs A)
 			}
 			const int nit = wave_max_i32(c_hi - c_lo);
 			uint32_t tl = 0;
-			scan_any<K, true>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl, lane);
+			scan_any<K, true, ABL>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl, lane);
 			tally += tl;
 		}
 	}
@@ -969,7 +1019,7 @@ static hipError_t launch_kw(const VcKernelArgs *A, int grid, int grid_long, hipS
 	hipLaunchKernelGGL((vc_count_reads_kernel<K, ABL>), dim3(grid), dim3(VC_BLOCK), lds, st, *A);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return e;
-	hipLaunchKernelGGL((vc_count_long_kernel<K>), dim3(grid_long), dim3(VC_BLOCK), lds, st, *A);
+	hipLaunchKernelGGL((vc_count_long_kernel<K, ABL & VC_KV_FLANK>), dim3(grid_long), dim3(VC_BLOCK), lds, st, *A);
 	return hipGetLastError();
 }
 
@@ -983,13 +1033,18 @@ static hipError_t launch_k(const VcKernelArgs *A, int grid, int grid_long, hipSt
 #ifdef VC_ABLATION
 	if constexpr (K == 21) {
 		if (A->ablate) switch (A->ablate) {
-#define VC_ABL_CASE(n) case n: return launch_kw<21, n>(A, grid, grid_long, st);
+#define VC_ABL_CASE(n)                                                                          \
+	case n:                                                                                     \
+		return A->flank ? launch_kw<21, n | VC_KV_FLANK>(A, grid, grid_long, st)                \
+		                : launch_kw<21, n>(A, grid, grid_long, st);
 			VC_ABL_LIST(VC_ABL_CASE)
 #undef VC_ABL_CASE
 		default: break;
 		}
 	}
 #endif
+	if constexpr (K >= VC_FLANK_MIN_K)
+		if (A->flank) return launch_kw<K, VC_KV_FLANK>(A, grid, grid_long, st);
 	return launch_kw<K>(A, grid, grid_long, st);
 }
 
@@ -1001,11 +1056,22 @@ static hipError_t setup_k(int lds)
 	if (e == hipSuccess)
 		e = hipFuncSetAttribute((const void *)vc_count_long_kernel<K>,
 		                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+	if constexpr (K >= VC_FLANK_MIN_K) {
+		if (e == hipSuccess)
+			e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<K, VC_KV_FLANK>,
+			                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+		if (e == hipSuccess)
+			e = hipFuncSetAttribute((const void *)vc_count_long_kernel<K, VC_KV_FLANK>,
+			                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+	}
 #ifdef VC_ABLATION
 	if constexpr (K == 21) {
 #define VC_ABL_SET(n)                                                                           \
 	if (e == hipSuccess)                                                                        \
 		e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<21, n>,                     \
+		                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);               \
+	if (e == hipSuccess)                                                                        \
+		e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<21, n | VC_KV_FLANK>,       \
 		                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 		VC_ABL_LIST(VC_ABL_SET)
 #undef VC_ABL_SET

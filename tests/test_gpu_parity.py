@@ -134,6 +134,42 @@ def test_random_reads_vs_oracle(k):
     assert int(want.sum()) > 0
 
 
+@pytest.mark.parametrize("filt", ["bloom", "flank"])
+@pytest.mark.parametrize("k", [21, 22, 26, 27, 31])
+def test_prefilter_modes_vs_oracle(k, filt):
+    """Both LDS prefilters (VAFC_FILTER: the Bloom filter, the flank bitmap of
+    vafc_common.h) count identically to the oracle, whole and long reads
+    (the long-read kernel's segments start mid-read), with keys that occur."""
+    rng = np.random.default_rng(500 + k)
+    lens = list(rng.integers(0, 400, 2500)) + [k - 1, k, k + 1, 30, 31, 32, 33, 47, 48, 49, 150, 16384, 16400, 40000]
+    reads = random_reads(rng, lens)
+    keys, vals, n_pat = table_from_reads(k, reads, rng, n_pat=3000)
+    got, km = gpu_counts(k, keys, vals, n_pat, reads, blocks=2, env={"VAFC_FILTER": filt})
+    want, km_want = oracle_counts(k, keys, vals, n_pat, reads)
+    assert km == km_want
+    assert np.array_equal(got, want)
+    assert int(want.sum()) > 200
+
+
+@pytest.mark.parametrize("k", [21, 31])
+def test_every_kmer_of_golden_reads_flank(k):
+    """The flank bitmap forced on with a dense key set (every k-mer of the golden
+    reads): a necessary-condition filter may pass more, never fewer."""
+    import oracle as O
+    z = np.load(os.path.join(GOLDEN, "kmers_k%d.npz" % k))
+    seq, lens = z["seq"], z["lens"]
+    reads, pos = [], 0
+    for L in lens:
+        reads.append(seq[pos:pos + int(L)].tobytes())
+        pos += int(L)
+    allk = np.concatenate([O.read_kmers(k, r) for r in reads])
+    uniq, mult = np.unique(allk, return_counts=True)
+    vals = np.arange(uniq.size, dtype=np.uint32)
+    got, km = gpu_counts(k, uniq, vals, (uniq.size + 1) // 2, reads, env={"VAFC_FILTER": "flank"})
+    assert km == allk.size
+    assert np.array_equal(got[: uniq.size], mult.astype(np.uint32))
+
+
 @pytest.mark.parametrize("k", [21, 31, 9, 16, 26])
 def test_long_reads_segmented_kernel(k):
     """Reads > VC_LONG_READ (16384) take the segmented long-read kernel."""
