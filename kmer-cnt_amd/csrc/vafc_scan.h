@@ -863,18 +863,128 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	}
 }
 
-// k in 16..31 with a compile-time specialisation: packed streams; otherwise
-// the general rolling scan.
+// The same scan with chunks in quads: each lane requests the next 64 bytes of
+// its read (four dwordx4 from one or two lines, back to back) while the
+// current four chunks are scanned.  Every lane of a wave reads a different
+// read, so every request misses the 32 KiB L1 (16 waves x 64 lanes keep
+// 128 KiB of lines live); the L1's outstanding misses, not instruction issue,
+// bound the pair loop once the flank prefilter cut the VALU per base
+// (TCP_PENDING_STALL_CYCLES 70 % of the kernel).  Four requests to one line
+// back to back cost it one miss instead of two.  A.variant bit 3 selects the
+// pair loop (A/B).
+template <int K, bool HAS_LO, int ABL = 0, bool SAFE = false>
+__device__ __forceinline__ void scan_span_quad(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
+                                               uint64_t wmax, uint64_t off, int len, int c_lo, int vlo, int vhi,
+                                               int nit, const uint32_t *__restrict__ filt, WaveQueue &Q,
+                                               uint32_t &tl, int lane)
+{
+	if (nit == 0) return;            // wave-uniform; the loads below assume a chunk
+	const int tail_c = A.nt4 ? -1 : ((len & 15) ? (len >> 4) : -1);
+	const int nt4m = -(int)A.nt4;
+	const uint64_t addr = off + 16ull * (uint64_t)c_lo;
+	uint64_t wi = addr >> 2;
+	const uint32_t sh = (uint32_t)(addr & 3u);
+	uint32_t w[17], d[4];
+	w[0] = SAFE ? s32[wi] : ldw(s32, wi, wmax);
+#pragma unroll
+	for (int q = 0; q < 4; ++q) d[q] = ldq_s<SAFE>(s32, wi + 1 + 4 * q, wmax, w[4 * q + 1], w[4 * q + 2], w[4 * q + 3], w[4 * q + 4]);
+	constexpr bool PEEL = !HAS_LO && K >= 17 && (ABL & 32) == 0;
+	[[maybe_unused]] uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0, dx = 0;
+	if constexpr (PEEL) dx = ldq_s<SAFE>(s32, wi + 17, wmax, x0, x1, x2, x3);
+
+	uint32_t Bm1 = 0, Bm2 = 0, Cm1 = 0, Cm2 = 0, H = 0;
+	int U = 1 - K - vlo + 16 * c_lo;
+	int Qe = -vhi + 16 * c_lo;
+	int it = 0;
+	// chunk 0 of a whole read builds only the streams (see scan_span_packed);
+	// the quads then start at chunk 1, chunk 4's dwords requested up front
+	if constexpr (PEEL) {
+		if ((A.variant & 1u) == 0) {
+			quad_fix(d[0], w[1], w[2], w[3], w[4]);
+			packed_streams<K, ABL>(c_lo, tail_c, nt4m, sh, w[0], w[1], w[2], w[3], w[4], Bm1, Bm2, Cm1, Cm2, U, Qe, H,
+			                       filt);
+#pragma unroll
+			for (int i = 0; i < 13; ++i) w[i] = w[i + 4];
+			w[13] = x0; w[14] = x1; w[15] = x2; w[16] = x3;
+			d[0] = d[1]; d[1] = d[2]; d[2] = d[3]; d[3] = dx;
+			wi += 4;
+			it = 1;
+		}
+	}
+	auto chunk = [&](auto j0tag, auto j1tag, int c, int b) {
+		packed_chunk<K, ABL, decltype(j0tag)::value, decltype(j1tag)::value>(
+			A, c, tail_c, nt4m, sh, w[b], w[b + 1], w[b + 2], w[b + 3], w[b + 4], Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q,
+			tl, lane);
+	};
+	auto trip = [&](auto j0tag) {
+		const int c = c_lo + it;
+		uint32_t n[16], dn[4];
+#pragma unroll
+		for (int q = 0; q < 4; ++q)
+			dn[q] = ldq_s<SAFE>(s32, wi + 17 + 4 * q, wmax, n[4 * q], n[4 * q + 1], n[4 * q + 2], n[4 * q + 3]);
+#pragma unroll
+		for (int q = 0; q < 4; ++q) quad_fix(d[q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3], w[4 * q + 4]);
+		chunk(j0tag, J0Tag<16>{}, c, 0);
+		chunk(J0Tag<0>{}, J0Tag<16>{}, c + 1, 4);
+		chunk(J0Tag<0>{}, J0Tag<16>{}, c + 2, 8);
+		chunk(J0Tag<0>{}, J0Tag<16>{}, c + 3, 12);
+		w[0] = w[16];
+#pragma unroll
+		for (int i = 0; i < 16; ++i) w[i + 1] = n[i];
+#pragma unroll
+		for (int q = 0; q < 4; ++q) d[q] = dn[q];
+		wi += 16;
+	};
+	if constexpr (!HAS_LO && K >= 18 && (ABL & 32) == 0 && (ABL & VC_KV_FLANK) == 0) {
+		if (it == 1 && it + 4 < nit && (A.variant & 2u) == 0) {
+			trip(J0Tag<K - 17>{});
+			it += 4;
+		}
+	}
+	for (; it + 4 < nit; it += 4) trip(J0Tag<0>{});
+	// the last 1..4 chunks, all in w already (wave-uniform count)
+#pragma unroll
+	for (int q = 0; q < 4; ++q) quad_fix(d[q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3], w[4 * q + 4]);
+	const int r = nit - it;
+	if (r >= 2) chunk(J0Tag<0>{}, J0Tag<16>{}, c_lo + it, 0);
+	if (r >= 3) chunk(J0Tag<0>{}, J0Tag<16>{}, c_lo + it + 1, 4);
+	if (r >= 4) chunk(J0Tag<0>{}, J0Tag<16>{}, c_lo + it + 2, 8);
+	// the wave's last chunk: only its lower 8 windows when no lane has more
+	// valid ones (see scan_span_packed)
+	const int b = 4 * (r - 1);
+	if (b != 0) {
+		w[0] = b == 4 ? w[4] : (b == 8 ? w[8] : w[12]);
+		w[1] = b == 4 ? w[5] : (b == 8 ? w[9] : w[13]);
+		w[2] = b == 4 ? w[6] : (b == 8 ? w[10] : w[14]);
+		w[3] = b == 4 ? w[7] : (b == 8 ? w[11] : w[15]);
+		w[4] = b == 4 ? w[8] : (b == 8 ? w[12] : w[16]);
+	}
+	const int cl = c_lo + nit - 1;
+	if ((A.variant & 4u) == 0 && __ballot(vhi - 16 * cl > 8) == 0)
+		chunk(J0Tag<0>{}, J0Tag<8>{}, cl, 0);
+	else
+		chunk(J0Tag<0>{}, J0Tag<16>{}, cl, 0);
+}
+
+// k in 16..31 with a compile-time specialisation: packed streams (the quad
+// loop unless A.variant bit 3 or a memory ablation); otherwise the general
+// rolling scan.
 template <int K, bool HAS_LO, int ABL = 0, bool SAFE = false>
 __device__ __forceinline__ void scan_any(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
                                          uint64_t wmax, uint64_t off, int len, int c_lo, int c_hi,
                                          int vlo, int vhi, int nit, const uint32_t *__restrict__ filt,
                                          WaveQueue &Q, uint32_t &tl, int lane)
 {
-	if constexpr (K >= 16)
+	if constexpr (K >= 16) {
+		if constexpr ((ABL & (2 | 8 | 16)) == 0) {
+			if ((A.variant & 8u) == 0) {
+				scan_span_quad<K, HAS_LO, ABL, SAFE>(A, s32, wmax, off, len, c_lo, vlo, vhi, nit, filt, Q, tl, lane);
+				return;
+			}
+		}
 		scan_span_packed<K, HAS_LO, ABL, SAFE>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl,
 		                                       lane);
-	else
+	} else
 		scan_span<K, HAS_LO, ABL>(A, s32, wmax, off, len, c_lo, c_hi, vlo, vhi, nit, filt, Q, tl, lane);
 }
 
