@@ -542,8 +542,8 @@ __device__ __forceinline__ uint32_t flank_bits(uint32_t fbase, uint32_t Bm1, uin
 // One 16-base chunk c of the packed scan from its five dwords (w0: the dword
 // holding the chunk's first byte, realigned by sh); (B1, C1) / (B2, C2) are
 // the streams of chunks c-1 / c-2 and move on to c / c-1.
-template <int K, int ABL, int J0 = 0, int J1 = 16>
-__device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int tail_c, int nt4m, uint32_t sh,
+template <int K, int ABL, int J0 = 0, int J1 = 16, bool DEFER = false>
+__device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, int tail_c, int nt4m, uint32_t sh,
                                              uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
                                              uint32_t &Bm1, uint32_t &Bm2, uint32_t &Cm1, uint32_t &Cm2,
                                              int &U, int &Qe, uint32_t &H, const uint32_t *__restrict__ filt,
@@ -622,8 +622,13 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 	}
 	hm &= V;
 	tl += (uint32_t)__builtin_popcount(V);
-	// queue the hit positions' forward k-mers (bit b <-> base j = 15 - b)
-	if constexpr ((ABL & 4) != 0) {
+	// queue the hit positions' forward k-mers (bit b <-> base j = 15 - b);
+	// DEFER: the caller runs one hit loop for two chunks (hit_loop2)
+	if constexpr (DEFER) {
+		Bm2 = Bm1; Bm1 = Bc;
+		Cm2 = Cm1; Cm1 = Cc;
+		return hm;
+	} else if constexpr ((ABL & 4) != 0) {
 		asm volatile("" :: "v"(hm));
 	} else if (__ballot(hm != 0u)) {
 		for (;;) {
@@ -640,6 +645,38 @@ __device__ __forceinline__ void packed_chunk(const VcKernelArgs &A, int c, int t
 	}
 	Bm2 = Bm1; Bm1 = Bc;
 	Cm2 = Cm1; Cm1 = Cc;
+	return 0u;
+}
+
+// One hit loop for two consecutive chunks a, a + 1 (packed_chunk<DEFER>):
+// hm = (hm_a << 16) | hm_a+1, streams B[a-2] .. B[a+1].  A trip takes every
+// lane's lowest pass; a lane's passes in 32 windows need fewer trips than in
+// two separate 16-window loops (about 1.7 against 2.5 per chunk pair at the
+// benchmark panel's pass rate), at 4 VALU per trip to pick the chunk's
+// streams.  v_alignbit uses the low 5 bits of its shift, so 2b serves both
+// halves.
+template <int K, int ABL>
+__device__ __forceinline__ void hit_loop2(const VcKernelArgs &A, WaveQueue &Q, uint32_t hm, uint32_t Bam2,
+                                          uint32_t Bam1, uint32_t Ba, uint32_t Bb, int lane)
+{
+	constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
+	if constexpr ((ABL & 4) != 0) {
+		asm volatile("" :: "v"(hm));
+	} else if (__ballot(hm != 0u)) {
+		for (;;) {
+			const bool has = hm != 0u;
+			const uint64_t bal = __ballot(has);
+			if (!bal) break;
+			uint32_t b;   // lowest pass; lanes without one get ~0 and append nothing
+			asm("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(hm));
+			const bool ina = b >= 16u;
+			const uint32_t lo = ina ? Ba : Bb, hi = ina ? Bam1 : Ba, hi2 = ina ? Bam2 : Bam1;
+			const uint32_t flo = __builtin_amdgcn_alignbit(hi, lo, 2u * b);
+			const uint32_t fhi = __builtin_amdgcn_alignbit(hi2, hi, 2u * b) & HIM;
+			queue_append(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
+			hm &= hm - 1u;
+		}
+	}
 }
 
 // Chunk c's streams only, for a chunk in which no window can be valid (chunk
@@ -916,6 +953,11 @@ __device__ __forceinline__ void scan_span_quad(const VcKernelArgs &A, const uint
 			A, c, tail_c, nt4m, sh, w[b], w[b + 1], w[b + 2], w[b + 3], w[b + 4], Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q,
 			tl, lane);
 	};
+	auto dchunk = [&](auto j0tag, int c, int b) -> uint32_t {
+		return packed_chunk<K, ABL, decltype(j0tag)::value, 16, true>(
+			A, c, tail_c, nt4m, sh, w[b], w[b + 1], w[b + 2], w[b + 3], w[b + 4], Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q,
+			tl, lane);
+	};
 	auto trip = [&](auto j0tag) {
 		const int c = c_lo + it;
 		uint32_t n[16], dn[4];
@@ -924,10 +966,28 @@ __device__ __forceinline__ void scan_span_quad(const VcKernelArgs &A, const uint
 			dn[q] = ldq_s<SAFE>(s32, wi + 17 + 4 * q, wmax, n[4 * q], n[4 * q + 1], n[4 * q + 2], n[4 * q + 3]);
 #pragma unroll
 		for (int q = 0; q < 4; ++q) quad_fix(d[q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3], w[4 * q + 4]);
-		chunk(j0tag, J0Tag<16>{}, c, 0);
-		chunk(J0Tag<0>{}, J0Tag<16>{}, c + 1, 4);
-		chunk(J0Tag<0>{}, J0Tag<16>{}, c + 2, 8);
-		chunk(J0Tag<0>{}, J0Tag<16>{}, c + 3, 12);
+		// flank mode: one hit loop per chunk pair (the Bloom-filter kernels are
+		// at the 128-VGPR limit and would spill; ablation builds: A.variant
+		// bit 6 = per chunk)
+		bool defer = (ABL & VC_KV_FLANK) != 0;
+#ifdef VC_ABLATION
+		defer = defer && (A.variant & 64u) == 0;
+#endif
+		if constexpr ((ABL & VC_KV_FLANK) == 0) defer = false;
+		if (defer) {
+#pragma unroll
+			for (int p = 0; p < 2; ++p) {
+				const uint32_t s2 = Bm2, s1 = Bm1;
+				uint32_t h = p == 0 ? dchunk(j0tag, c, 0) : dchunk(J0Tag<0>{}, c + 2, 8);
+				h = (h << 16) | dchunk(J0Tag<0>{}, c + 2 * p + 1, 8 * p + 4);
+				hit_loop2<K, ABL>(A, Q, h, s2, s1, Bm2, Bm1, lane);
+			}
+		} else {
+			chunk(j0tag, J0Tag<16>{}, c, 0);
+			chunk(J0Tag<0>{}, J0Tag<16>{}, c + 1, 4);
+			chunk(J0Tag<0>{}, J0Tag<16>{}, c + 2, 8);
+			chunk(J0Tag<0>{}, J0Tag<16>{}, c + 3, 12);
+		}
 		w[0] = w[16];
 #pragma unroll
 		for (int i = 0; i < 16; ++i) w[i + 1] = n[i];
@@ -977,7 +1037,10 @@ __device__ __forceinline__ void scan_any(const VcKernelArgs &A, const uint32_t *
 {
 	if constexpr (K >= 16) {
 		if constexpr ((ABL & (2 | 8 | 16)) == 0) {
-			if ((A.variant & 8u) == 0) {
+#ifdef VC_ABLATION
+			if ((A.variant & 8u) == 0)   // ablation builds: A.variant bit 3 = the pair loop
+#endif
+			{
 				scan_span_quad<K, HAS_LO, ABL, SAFE>(A, s32, wmax, off, len, c_lo, vlo, vhi, nit, filt, Q, tl, lane);
 				return;
 			}
