@@ -508,6 +508,23 @@ __device__ __forceinline__ uint32_t pack_codes(uint32_t t0, uint32_t t1, uint32_
 	return lo | hi;
 }
 
+// The big-endian stream pairrev(pack_codes(...)) directly (flank kernels,
+// which need no little-endian stream): multiplying by 2^30 + 2^20 + 2^10 + 1
+// puts code r of a dword at bit 30 - 2r of its top byte (the partial products
+// land in disjoint 2-bit fields: 8r + {0, 10, 20, 30}), i.e. the byte holds
+// its four codes reversed, and the perms place dword m's byte at byte 3 - m.
+// Saves the 4-VALU pair reversal per chunk.
+__device__ __forceinline__ uint32_t pack_codes_rev(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3)
+{
+	const uint32_t g0 = (t0 & 0x03030303u) * 0x40100401u;
+	const uint32_t g1 = (t1 & 0x03030303u) * 0x40100401u;
+	const uint32_t g2 = (t2 & 0x03030303u) * 0x40100401u;
+	const uint32_t g3 = (t3 & 0x03030303u) * 0x40100401u;
+	const uint32_t lo = __builtin_amdgcn_perm(g2, g3, 0x0C0C0703u);   // bytes 0, 1: g3, g2 top bytes
+	const uint32_t hi = __builtin_amdgcn_perm(g0, g1, 0x07030C0Cu);   // bytes 2, 3: g1, g0 top bytes
+	return lo | hi;
+}
+
 __device__ __forceinline__ int clamp16(int v) { return v < 0 ? 0 : (v > 16 ? 16 : v); }
 
 // Flank-bitmap lookups of one chunk (VC_KV_FLANK): R with bit 15 - j set iff
@@ -564,9 +581,10 @@ __device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, i
 	}
 	U += 16;
 	Qe += 16;
-	const uint32_t L = pack_codes(t0, t1, t2, t3);  // base j at bits 2j
-	const uint32_t Cc = ~L;                          // complement codes, little-endian
-	const uint32_t Bc = pairrev(L);                  // big-endian codes
+	constexpr bool FL = (ABL & VC_KV_FLANK) != 0;
+	const uint32_t L = FL ? 0u : pack_codes(t0, t1, t2, t3);  // base j at bits 2j
+	const uint32_t Cc = ~L;                          // complement codes, little-endian (unused by FL)
+	const uint32_t Bc = FL ? pack_codes_rev(t0, t1, t2, t3) : pairrev(L);   // big-endian codes
 
 	uint32_t hm = 0;                                 // filter pass, bit 15 - j for base j
 	if constexpr ((ABL & VC_KV_FLANK) != 0) {
@@ -701,7 +719,8 @@ __device__ __forceinline__ void packed_streams(int c, int tail_c, int nt4m, uint
 	}
 	U += 16;
 	Qe += 16;
-	const uint32_t L = pack_codes(t0, t1, t2, t3);
+	constexpr bool FL = (ABL & VC_KV_FLANK) != 0;
+	const uint32_t L = FL ? 0u : pack_codes(t0, t1, t2, t3);
 	const uint32_t anyinv = (t0 | t1 | t2 | t3) & 0x04040404u;
 	if (__ballot(anyinv != 0u)) {
 		if (anyinv != 0u) {   // as in packed_chunk: U moves to the last invalid base
@@ -713,7 +732,7 @@ __device__ __forceinline__ void packed_streams(int c, int tail_c, int nt4m, uint
 			U = U < u1 ? U : u1;
 		}
 	}
-	const uint32_t Bc = pairrev(L);
+	const uint32_t Bc = FL ? pack_codes_rev(t0, t1, t2, t3) : pairrev(L);
 	if constexpr ((ABL & VC_KV_FLANK) != 0) {
 		// the first window (ending at K - 1) starts with the 10-mer ending at
 		// base 9: chunk 0's bases 9..15 are looked up for the later windows
