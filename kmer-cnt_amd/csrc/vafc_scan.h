@@ -80,6 +80,16 @@ __device__ __forceinline__ uint32_t dec_head(uint32_t b)
 	return t | ((b >> 1) & 0x04040404u);
 }
 
+// The same without the byte-bit-3 term: codes, and bit 2 for the nibbles the
+// LUT marks invalid.  The packed scan tests bit 3 of the raw bytes once per
+// chunk instead of once per dword (dec_bit3) and folds it in only on the rare
+// invalid-base path.
+__device__ __forceinline__ uint32_t dec_code(uint32_t b)
+{
+	return __builtin_amdgcn_perm(NIB_HI, NIB_LO, b & 0x07070707u);
+}
+__device__ __forceinline__ uint32_t dec_bit3(uint32_t b) { return (b >> 1) & 0x04040404u; }
+
 // Tail decode = seq_nt4_table (vaf-counter.c:73-90) on 4 bytes: ACGTU/acgtu
 // keep their nibble code, bytes 0..3 map to themselves, all else invalid.
 __device__ __forceinline__ uint32_t dec_tail(uint32_t b)
@@ -574,7 +584,7 @@ __device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, i
 	const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
 	const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
 	const uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
-	uint32_t t0 = dec_head(b0), t1 = dec_head(b1), t2 = dec_head(b2), t3 = dec_head(b3);
+	uint32_t t0 = dec_code(b0), t1 = dec_code(b1), t2 = dec_code(b2), t3 = dec_code(b3);
 	const int cm = c | nt4m;
 	if (__ballot(cm == tail_c)) {
 		if (cm == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
@@ -624,9 +634,10 @@ __device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, i
 	}
 	// windows of this chunk inside [vlo, vhi) with no earlier invalid base
 	uint32_t V = ((1u << clamp16(U)) - 1u) & ~((1u << clamp16(Qe)) - 1u);
-	const uint32_t anyinv = (t0 | t1 | t2 | t3) & 0x04040404u;
+	const uint32_t anyinv = ((t0 | t1 | t2 | t3) & 0x04040404u) | ((b0 | b1 | b2 | b3) & 0x08080808u);
 	if (__ballot(anyinv != 0u)) {
 		if (anyinv != 0u) {
+			t0 |= dec_bit3(b0); t1 |= dec_bit3(b1); t2 |= dec_bit3(b2); t3 |= dec_bit3(b3);
 			// invalid flags packed like the codes: base j at bit 2j of F
 			const uint32_t Im = ((t0 >> 2) & 0x01010101u) | (t1 & 0x04040404u) |
 			                    ((t2 << 2) & 0x10101010u) | ((t3 << 4) & 0x40404040u);
@@ -712,7 +723,7 @@ __device__ __forceinline__ void packed_streams(int c, int tail_c, int nt4m, uint
 	const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
 	const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
 	const uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
-	uint32_t t0 = dec_head(b0), t1 = dec_head(b1), t2 = dec_head(b2), t3 = dec_head(b3);
+	uint32_t t0 = dec_code(b0), t1 = dec_code(b1), t2 = dec_code(b2), t3 = dec_code(b3);
 	const int cm = c | nt4m;
 	if (__ballot(cm == tail_c)) {
 		if (cm == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
@@ -721,9 +732,10 @@ __device__ __forceinline__ void packed_streams(int c, int tail_c, int nt4m, uint
 	Qe += 16;
 	constexpr bool FL = (ABL & VC_KV_FLANK) != 0;
 	const uint32_t L = FL ? 0u : pack_codes(t0, t1, t2, t3);
-	const uint32_t anyinv = (t0 | t1 | t2 | t3) & 0x04040404u;
+	const uint32_t anyinv = ((t0 | t1 | t2 | t3) & 0x04040404u) | ((b0 | b1 | b2 | b3) & 0x08080808u);
 	if (__ballot(anyinv != 0u)) {
 		if (anyinv != 0u) {   // as in packed_chunk: U moves to the last invalid base
+			t0 |= dec_bit3(b0); t1 |= dec_bit3(b1); t2 |= dec_bit3(b2); t3 |= dec_bit3(b3);
 			const uint32_t Im = ((t0 >> 2) & 0x01010101u) | (t1 & 0x04040404u) |
 			                    ((t2 << 2) & 0x10101010u) | ((t3 << 4) & 0x40404040u);
 			const uint32_t F = transpose2x4x4(Im);
