@@ -6,6 +6,12 @@ its own files) into a per-GPU uint32 count vector, and ONE all-reduce sums the
 vectors before rank 0 writes the .vaf.  With the "nccl" backend this is RCCL
 over xGMI; on CPU (tests) it is gloo.
 
+This module is only the one-process-per-GPU (torchrun) side used by bench.py
+and tests/test_synth_dist.py.  The product path for the drop-in CLI is
+in-process: vc_create_multi (include/vafc.h) holds one table replica and
+count vector per device and reduces them with RCCL inside vc_finish
+(DESIGN.md §6).
+
 uint32 counts are carried as int32 tensors: two's-complement addition is
 addition modulo 2^32, so the reduced vector is bit-identical to the
 reference's single-process uint32 counters (vaf-counter.c:101-102,473-477),
