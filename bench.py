@@ -464,7 +464,7 @@ def main():
                 "traffic": traffic,
                 "kernel": "vc_count_reads_kernel (+ vc_count_long_kernel, empty here)",
                 "limiter": "the roofline is HBM (integer byte work, no MFMA); the kernel runs below it, "
-                           "co-limited by VALU issue (11.7 VALU per base with the flank prefilter) and the L1 "
+                           "co-limited by VALU issue (11.4 VALU per base with the flank prefilter) and the L1 "
                            "miss path of one-read-per-lane loads (TCP pending-miss stalls); DESIGN.md section 3.1, "
                            "profiles/r02_quad_pmc/, profiles/r02_flank_ablation*.log",
                 "kernel_ms": round(k_ms, 4),
