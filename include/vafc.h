@@ -151,14 +151,18 @@ int vc_table_info(const vc_ctx *ctx, uint64_t *n_keys, uint64_t *slots, uint64_t
  * device may repeat: several shards on one GPU).  Host reads given to
  * vc_count_block / vc_count_file are dealt to the shards batch by batch,
  * round robin (the -b block loop and its stop rule still run once, in file
- * order); vc_count_device counts on shard 0 only.  vc_finish reduces the
- * shards -- same-device shards summed on their device, then one RCCL reduce
- * (ncclSum of the u32 counts and the u64 k-mer tally) to shard 0 over xGMI,
- * librccl.so.1 loaded on first use -- and returns the totals, bit-identical
+ * order); vc_count_device deals device batches the same way over the
+ * shards that live on the device holding d_seq (VC_EINVAL if none does).
+ * vc_finish reduces the shards -- same-device shards summed on their device,
+ * then, when the shards span more than one device, one RCCL reduce (ncclSum
+ * of the u32 counts and the u64 k-mer tally) to shard 0 over xGMI -- and
+ * returns the totals, bit-identical
  * to a single device counting everything (u32 sums wrap like the
  * reference's counters).  vc_reset / vc_set_nt4_decode apply to every shard;
  * vc_bind_outputs, vc_device_counts, timing and vc_table_info to shard 0.
- * n_devices == 1 is vc_create. */
+ * n_devices == 1 is vc_create.  With more than one distinct device,
+ * librccl.so.1 ($VAFC_RCCL_LIB names another) is loaded before any device is
+ * touched; if it cannot be loaded the call fails with VC_EHIP. */
 int vc_create_multi(vc_ctx **out, int k, const uint64_t *keys, const uint32_t *vals, size_t n_keys,
                     uint32_t n_patterns, const int *devices, int n_devices);
 /* Shards of a counter (1 for vc_create), and shard i's device and the host
@@ -378,6 +382,11 @@ int vc_debug_decode(const uint8_t *d_seq, size_t seq_bytes, const uint64_t *d_of
 
 const char *vc_strerror(int err);
 int vc_version(void);
+/* Hash of the sources this library was built from (16 hex digits: sha256 of
+ * every file of kmer-cnt_amd/csrc in name order, then include/vafc.h).  The same string
+ * is embedded as "VAFC_BUILD_ID=<hex>" in the library and every CLI, so a
+ * checker can compare it with the tree without loading the binary. */
+const char *vc_build_id(void);
 
 #ifdef __cplusplus
 }

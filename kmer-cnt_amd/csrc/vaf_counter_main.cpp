@@ -105,7 +105,6 @@ int main(int argc, char *argv[])
 	rc = vc_create_multi(&ctx, k, keys, vals, n_keys, (uint32_t)n, devices.data(), (int)devices.size());
 	vc_free(keys);
 	vc_free(vals);
-	if (rc == VC_OK) rc = vc_reserve_file_ingest(ctx, n_thread);   // reader buffers, outside the counting timer
 	if (rc != VC_OK) {
 		fprintf(stderr, "Error: failed to create k-mer map (%s)\n", vc_strerror(rc));
 		vc_destroy(ctx);
@@ -120,6 +119,15 @@ int main(int argc, char *argv[])
 
 	fprintf(stderr, "[M::%s] Counting k-mers in FASTQ files with %d threads...\n", "main", n_thread);
 	t = now_s();
+	// the reader's pinned buffers are allocated inside the counting timer, as
+	// the reference allocates its per-block buffers inside it (vaf-counter.c:489-503)
+	rc = vc_reserve_file_ingest(ctx, n_thread);
+	if (rc != VC_OK) {
+		fprintf(stderr, "Error: counting failed (%s)\n", vc_strerror(rc));
+		vc_destroy(ctx);
+		vc_patterns_free(db);
+		return 1;
+	}
 	uint64_t tot_bases = 0, tot_seqs = 0;
 	for (int i = optind; i < argc; ++i) {
 		fprintf(stderr, "[M::%s] Processing %s...\n", "main", argv[i]);

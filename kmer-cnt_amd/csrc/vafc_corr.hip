@@ -43,6 +43,8 @@
 
 #include <atomic>
 #include <new>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <string>
 #include <vector>
@@ -315,28 +317,61 @@ extern "C" int vc_vafset_add_many(vc_vafset *s, const char *const *paths, int n,
 	std::vector<std::vector<double>> x(n);
 	std::vector<std::vector<int32_t>> d(n);
 	std::vector<char> tr(n, 0);
-	// the files are opened here, in order, up to the first that cannot be
-	// opened, as the reference's loop does (nothing after it is opened: a
-	// FIFO named after a missing file must not block); workers read them
-	std::vector<FILE *> fp;
-	for (int i = 0; i < n; ++i) {
-		FILE *f = fopen(paths[i], "r");
-		if (!f) break;
-		fp.push_back(f);
-	}
-	const int m = (int)fp.size();
-	std::atomic<int> next(0);
+	// The files are opened here, in order, up to the first that cannot be
+	// opened, as the reference's loop does (correlation-matrix.c:304,329-335;
+	// nothing after it is opened: a FIFO named after a missing file must not
+	// block).  At most W files are open and not yet parsed at any time (the
+	// workers close each one once parsed), so any number of inputs works under
+	// the usual 1,024-descriptor limit, like the reference's one-at-a-time loop.
 	const int T = n_threads < 1 ? 1 : (n_threads > 64 ? 64 : n_threads);
+	const int W = 2 * T < 64 ? 2 * T : 64;
+	std::vector<FILE *> fp((size_t)n, nullptr);
+	std::mutex mu;
+	std::condition_variable cv;
+	int opened = 0, handed = 0, parsed = 0;
+	bool closed = false;                           // no more files will be opened
 	std::vector<std::thread> th;
-	for (int t = 0; t < T && t < m; ++t)
+	for (int t = 0; t < T && t < n; ++t)
 		th.emplace_back([&] {
-			for (int i; (i = next.fetch_add(1)) < m;) {
+			for (;;) {
+				int i;
+				{
+					std::unique_lock<std::mutex> lk(mu);
+					cv.wait(lk, [&] { return handed < opened || closed; });
+					if (handed >= opened) return;  // closed and nothing left
+					i = handed++;
+				}
 				bool trunc = false;
-				vaf_load_fp(fp[(size_t)i], paths[i], nm[i], x[i], d[i], trunc);
+				vaf_load_fp(fp[(size_t)i], paths[i], nm[i], x[i], d[i], trunc);   // closes the file
 				tr[i] = trunc;
+				{
+					std::lock_guard<std::mutex> lk(mu);
+					++parsed;
+				}
+				cv.notify_all();
 			}
 		});
+	for (int i = 0; i < n; ++i) {
+		{
+			std::unique_lock<std::mutex> lk(mu);
+			cv.wait(lk, [&] { return opened - parsed < W; });
+		}
+		FILE *f = fopen(paths[i], "r");
+		if (!f) break;
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			fp[(size_t)i] = f;
+			++opened;
+		}
+		cv.notify_all();
+	}
+	{
+		std::lock_guard<std::mutex> lk(mu);
+		closed = true;
+	}
+	cv.notify_all();
 	for (auto &t : th) t.join();
+	const int m = opened;
 	int i = 0;
 	for (; i < m; ++i) {                           // in order, up to the first file that failed
 		truncated[i] = (uint8_t)tr[i];

@@ -618,6 +618,22 @@ extern "C" int vc_count_device(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes
                                void *stream)
 {
 	if (!c || (n_reads && (!d_seq || !d_offs || !d_lens))) return VC_EINVAL;
+	if (!c->rep.empty() && n_reads) {
+		// a multi-shard counter deals device batches round robin, like host
+		// batches, over the shards that live on the device holding the reads
+		int d = c->dev;
+		hipPointerAttribute_t at;
+		if (hipPointerGetAttributes(&at, d_seq) == hipSuccess && at.type == hipMemoryTypeDevice) d = at.device;
+		(void)hipGetLastError();   // a host pointer is not an error here
+		vc_ctx *sh = nullptr;
+		for (int i = 0; i < n_shards(c) && !sh; ++i) {
+			vc_ctx *x = next_shard(c);
+			if (x->dev == d) sh = x;
+		}
+		if (!sh) return VC_EINVAL;
+		c = sh;
+		++c->batches;
+	}
 	HIPCK(hipSetDevice(c->dev));
 	return launch(c, d_seq, seq_bytes, d_offs, d_lens, n_reads,
 	              stream ? (hipStream_t)stream : c->st);
@@ -700,7 +716,9 @@ extern "C" int vc_finish(vc_ctx *c, uint32_t *counts, uint64_t *kmers)
 			vc_ctx *sh = shard_at(c, i);
 			uint32_t f = 0;
 			HIPCK(hipSetDevice(sh->dev));
-			HIPCK(hipStreamSynchronize(sh->st));
+			// the whole device: vc_count_device may have launched on a caller
+			// stream that does not synchronise with the shard's own
+			HIPCK(hipDeviceSynchronize());
 			HIPCK(hipMemcpy(&f, sh->d_flags, sizeof f, hipMemcpyDeviceToHost));
 			if (f & 1u) {
 				fprintf(stderr, "[E::vafc] more reads longer than %d bases than the long-read list holds "
@@ -829,8 +847,11 @@ const RcclApi *rccl()
 	std::lock_guard<std::mutex> lk(g_rccl_mu);
 	if (g_rccl.tried) return g_rccl.ok ? &g_rccl : nullptr;
 	g_rccl.tried = true;
-	void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-	if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+	// VAFC_RCCL_LIB names another library (tests point it at a missing file
+	// to exercise the RCCL-missing path)
+	const char *env = getenv("VAFC_RCCL_LIB");
+	void *h = dlopen(env && *env ? env : "librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+	if (!h && !(env && *env)) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
 	if (!h) {
 		fprintf(stderr, "[E::vafc] cannot load RCCL: %s\n", dlerror());
 		return nullptr;
@@ -874,6 +895,16 @@ extern "C" int vc_create_multi(vc_ctx **out, int k, const uint64_t *keys, const 
 {
 	if (!out || !devices || n_devices < 1 || n_devices > VC_MAX_SHARDS) return VC_EINVAL;
 	*out = nullptr;
+	// RCCL is needed only to reduce across distinct devices (shards that share
+	// a device are summed on it); load it before any device is touched, so a
+	// missing library fails fast and leaves nothing to free
+	int n_distinct = 0;
+	for (int i = 0; i < n_devices; ++i) {
+		bool seen = false;
+		for (int j = 0; j < i; ++j) seen = seen || devices[j] == devices[i];
+		n_distinct += seen ? 0 : 1;
+	}
+	if (n_distinct > 1 && !rccl()) return VC_EHIP;
 	vc_ctx *c = nullptr;
 	int rc = vc_create(&c, k, keys, vals, n_keys, n_patterns, devices[0]);
 	if (rc != VC_OK) return rc;
@@ -893,13 +924,9 @@ extern "C" int vc_create_multi(vc_ctx **out, int k, const uint64_t *keys, const 
 			}
 		c->lead.push_back(l);
 	}
-	if (n_devices > 1) {
+	if (n_distinct > 1) {
 		// one RCCL rank per distinct device; rank 0 is shard 0 (the reduce root)
 		const RcclApi *R = rccl();
-		if (!R) {
-			vc_destroy(c);
-			return VC_EHIP;
-		}
 		std::vector<int> devs;
 		for (int i = 0; i < n_devices; ++i)
 			if (c->lead[(size_t)i] == i) {
@@ -939,15 +966,33 @@ static int reduce_shards(vc_ctx *c)
 		HIPCK(hipSetDevice(L->dev));
 		HIPCK(vc_launch_shard_add(L->d_counts, S->d_counts, n, L->d_tally, S->d_tally, L->st));
 	}
+	if (c->comms.size() <= 1) {   // one distinct device: the on-device sum is the whole sum
+		HIPCK(hipSetDevice(c->dev));
+		HIPCK(hipStreamSynchronize(c->st));
+		return VC_OK;
+	}
 	const RcclApi *R = rccl();
 	if (!R) return VC_EHIP;
 	NCCK(R, R->group_start());
-	for (size_t j = 0; j < c->comms.size(); ++j) {
+	// every enqueue goes in, and the group is always closed, before an error
+	// is returned: an open group would leave RCCL's thread-local state pending
+	// for the next collective or for ncclCommDestroy in vc_destroy
+	ncclResult_t first = ncclSuccess;
+	for (size_t j = 0; j < c->comms.size() && first == ncclSuccess; ++j) {
 		vc_ctx *L = shard_at(c, c->comm_shard[j]);
-		if (n) NCCK(R, R->reduce(L->d_counts, L->d_counts, n, ncclUint32, ncclSum, 0, c->comms[j], L->st));
-		NCCK(R, R->reduce(L->d_tally, L->d_tally, 1, ncclUint64, ncclSum, 0, c->comms[j], L->st));
+		(void)hipSetDevice(L->dev);   // the rank's device (its comm and stream live there)
+		// in place on every rank: sendbuff == recvbuff; non-root ranks' buffers
+		// are left as they were (zeroed below)
+		if (n) first = R->reduce(L->d_counts, L->d_counts, n, ncclUint32, ncclSum, 0, c->comms[j], L->st);
+		if (first == ncclSuccess)
+			first = R->reduce(L->d_tally, L->d_tally, 1, ncclUint64, ncclSum, 0, c->comms[j], L->st);
 	}
-	NCCK(R, R->group_end());
+	const ncclResult_t ge = R->group_end();
+	if (first == ncclSuccess) first = ge;
+	if (first != ncclSuccess) {
+		fprintf(stderr, "[E::vafc] RCCL reduce of the shard counts failed: %s\n", R->error_string(first));
+		return VC_EHIP;
+	}
 	for (size_t j = 1; j < c->comms.size(); ++j) {   // non-root ranks restart from zero
 		vc_ctx *L = shard_at(c, c->comm_shard[j]);
 		HIPCK(hipSetDevice(L->dev));

@@ -978,6 +978,9 @@ __device__ __forceinline__ void scan_span_quad(const VcKernelArgs &A, const uint
 			wi += 4;
 			it = 1;
 		}
+		// a wave whose reads all fit in one chunk (<= 16 bases) is done: the
+		// tail below assumes at least one chunk left (wave-uniform)
+		if (it == nit) return;
 	}
 	auto chunk = [&](auto j0tag, auto j1tag, int c, int b) {
 		packed_chunk<K, ABL, decltype(j0tag)::value, decltype(j1tag)::value>(

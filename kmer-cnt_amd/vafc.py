@@ -46,7 +46,7 @@ EXPORTS = (
     "vc_vafset_count",
     "vc_vafset_name", "vc_vafset_snps", "vc_corr_matrix", "vc_corr_matrix_raw", "vc_corr_write", "vc_corr_tree",
     "vc_synth_reads",
-    "vc_debug_decode", "vc_strerror", "vc_version",
+    "vc_debug_decode", "vc_strerror", "vc_version", "vc_build_id",
 )
 
 
@@ -157,6 +157,7 @@ def lib():
         "vc_debug_decode": (C.c_int, [P, C.c_size_t, P, P, C.c_uint64, P, P]),
         "vc_strerror": (C.c_char_p, [C.c_int]),
         "vc_version": (C.c_int, []),
+        "vc_build_id": (C.c_char_p, []),
     }
     older = "VAFC_LIB" in os.environ      # A/B against an older build: bind what it has
     for name, (res, args) in sig.items():
@@ -167,6 +168,51 @@ def lib():
         f.argtypes = args
     _lib = L
     return L
+
+
+def tree_build_id(root: str = None) -> str:
+    """The build id of the sources in this tree (the Makefile's BUILD_ID): the
+    first 16 hex digits of sha256 over every file of kmer-cnt_amd/csrc in name
+    order, then include/vafc.h."""
+    import hashlib
+    csrc = os.path.join(_HERE, "csrc")
+    root = root or os.path.dirname(_HERE)
+    h = hashlib.sha256()
+    for fn in sorted(os.listdir(csrc)):
+        p = os.path.join(csrc, fn)
+        if os.path.isfile(p):
+            with open(p, "rb") as f:
+                h.update(f.read())
+    with open(os.path.join(root, "include", "vafc.h"), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def binary_build_id(path: str):
+    """The "VAFC_BUILD_ID=<hex>" string embedded in a built binary (read from
+    the file, not loaded), or None."""
+    import re
+    try:
+        with open(path, "rb") as f:
+            m = re.search(rb"VAFC_BUILD_ID=([0-9a-f]{16})", f.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
+def check_build(paths=None) -> None:
+    """Raise VafcError unless every product binary carries the tree's build id."""
+    want = tree_build_id()
+    lib_dir = os.path.join(_HERE, "lib")
+    paths = paths or [os.path.join(lib_dir, f) for f in BINARIES]
+    bad = [(os.path.basename(p), binary_build_id(p)) for p in paths if binary_build_id(p) != want]
+    if bad:
+        raise VafcError("stale or missing build: the tree's sources hash to %s, but %s; "
+                        "rebuild with make -C kmer-cnt_amd/csrc" % (
+                            want, ", ".join("%s has %s" % (n, i) for n, i in bad)))
+
+
+BINARIES = ("libvafc.so", "vaf-counter", "snp-pattern-gen", "kc-c4", "yak-count", "correlation-matrix")
 
 
 def _ck(rc, what):

@@ -29,16 +29,20 @@ def built():
     jobs = str(min(8, os.cpu_count() or 2))
     subprocess.run(["make", "-s", "-j", jobs, "-C", os.path.join(ROOT, "oracle")], check=True)
     # The product is prebuilt in-tree (its objects do not travel to the GPU
-    # box, so make would rebuild it there from scratch): rebuild only when a
-    # library or CLI is missing or older than a source.
-    csrc = os.path.join(PKG, "csrc")
-    srcs = [os.path.join(csrc, f) for f in os.listdir(csrc)] + [os.path.join(ROOT, "include", "vafc.h")]
-    newest = max(os.path.getmtime(f) for f in srcs)
-    outs = [os.path.join(PKG, "lib", f) for f in ("libvafc.so", "vaf-counter", "snp-pattern-gen", "kc-c4",
-                                                  "yak-count", "correlation-matrix")]
-    if all(os.path.exists(f) and os.path.getmtime(f) >= newest for f in outs):
+    # box, so make would rebuild it there from scratch).  Every binary carries
+    # the hash of the sources it was built from (vc_build_id, the Makefile's
+    # BUILD_ID); it must equal the hash of this tree's sources.  Where the
+    # build host's reference tree is present, a mismatch rebuilds; elsewhere
+    # (the GPU box) it stops the session instead of testing a stale library.
+    import vafc
+    try:
+        vafc.check_build()
         return
-    subprocess.run(["make", "-s", "-j", jobs, "-C", csrc], check=True)
+    except vafc.VafcError as e:
+        if not os.path.isdir("/root/reference") and os.environ.get("VAFC_AUTO_BUILD") != "1":
+            pytest.exit(str(e), returncode=3)
+    subprocess.run(["make", "-s", "-j", jobs, "-C", os.path.join(PKG, "csrc")], check=True)
+    vafc.check_build()
 
 
 @pytest.fixture(scope="session")

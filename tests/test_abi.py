@@ -108,3 +108,53 @@ def test_reference_binding_patch_applies():
     spec.loader.exec_module(m)
     out = m.patch(open(src).read())
     assert out.count("vc_count_file(") == 1 and out.count("vc_create(") == 1 and "count_fastq_kmers(argv[i]" not in out
+
+
+def test_build_id_matches_tree():
+    """Every product binary carries the hash of the sources it was built from
+    ("VAFC_BUILD_ID=<hex>", vc_build_id); it equals the hash of this tree's
+    kmer-cnt_amd/csrc/* + include/vafc.h, so a stale binary cannot pass."""
+    import vafc
+    want = vafc.tree_build_id()
+    assert re.fullmatch(r"[0-9a-f]{16}", want)
+    vafc.check_build()
+    assert vafc.lib().vc_build_id().decode() == want
+
+
+def _lib_dir():
+    lib = os.environ.get("VAFC_LIB")
+    return os.path.dirname(lib) if lib else os.path.join(ROOT, "kmer-cnt_amd", "lib")
+
+
+def test_rccl_missing_fails_loudly(tmp_path):
+    """More than one distinct device and no loadable RCCL: vc_create_multi
+    returns VC_EHIP before any device is touched, and the CLI with
+    VAFC_DEVICES=0,1 exits 1 with the error (no GPU needed: RCCL is loaded
+    first).  Under tools/asan_tests.sh the CLI is the sanitizer build and runs
+    with leak detection on, so a leak on this path fails the test."""
+    import subprocess
+    import sys
+    import vafc
+    env = dict(os.environ, VAFC_RCCL_LIB="/nonexistent/librccl.so.1")
+    code = ("import sys, ctypes as C, numpy as np; sys.path.insert(0, %r); import vafc; L = vafc.lib(); "
+            "h = C.c_void_p(); k = np.zeros(1, np.uint64); v = np.zeros(1, np.uint32); "
+            "d = np.array([0, 1], np.int32); "
+            "print(L.vc_create_multi(C.byref(h), 21, k.ctypes.data_as(C.c_void_p), v.ctypes.data_as(C.c_void_p), "
+            "1, 1, d.ctypes.data_as(C.c_void_p), 2), h.value)" % os.path.join(ROOT, "kmer-cnt_amd"))
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.stdout.split() == [str(vafc.VC_EHIP), "None"], p.stdout
+    assert "cannot load RCCL" in p.stderr
+    pat = tmp_path / "p.txt"
+    pat.write_text("chr1\t1\t2\trs1\tA\tC\tACGTACGTACGTACGTACGTA\tACGTACGTACGAACGTACGTA\n")
+    fq = tmp_path / "r.fq"
+    fq.write_text("@r\nACGTACGTACGTACGTACGTACGT\n+\nIIIIIIIIIIIIIIIIIIIIIIII\n")
+    cli = os.path.join(_lib_dir(), "vaf-counter")
+    env2 = dict(env, VAFC_DEVICES="0,1")
+    if "asan" in env.get("LD_PRELOAD", ""):
+        env2["ASAN_OPTIONS"] = env.get("ASAN_OPTIONS", "").replace("detect_leaks=0", "detect_leaks=1")
+    p = subprocess.run([cli, "-p", str(pat), "-o", str(tmp_path / "o.vaf"), str(fq)], env=env2,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 1, p.stderr[-3000:]
+    assert "cannot load RCCL" in p.stderr and "failed to create k-mer map" in p.stderr
+    assert not (tmp_path / "o.vaf").exists()

@@ -219,6 +219,36 @@ def test_loader_parallel_matches_sequential(work, threads):
         S.close()
 
 
+_MANY_FILES = r"""
+import os, resource, sys
+sys.path.insert(0, sys.argv[1])
+import vafc
+vafc.lib()
+resource.setrlimit(resource.RLIMIT_NOFILE, (128, resource.getrlimit(resource.RLIMIT_NOFILE)[1]))
+d = sys.argv[2]
+fns = [os.path.join(d, "s%04d.vaf" % i) for i in range(int(sys.argv[3]))]
+S = vafc.VafSamples()
+assert S.load_vaf_files(fns, int(sys.argv[4])) == [False] * len(fns)
+assert [S.name(i) for i in range(len(S))] == ["s%04d" % i for i in range(len(fns))]
+assert all(S.n_snps(i) == 3 for i in range(len(S)))
+print("ok", len(S))
+"""
+
+
+@pytest.mark.parametrize("threads", [1, 8, 64])
+def test_loader_more_files_than_descriptors(tmp_path, threads):
+    """vc_vafset_add_many keeps a bounded window of open files: 600 inputs load
+    under a 128-descriptor limit (at most 64 open at once) (the reference opens and closes one file at a
+    time, correlation-matrix.c:304,329-335, so it has no such limit)."""
+    row = "chr1\t%d\trs%d\tA\tC\t5\t5\t10\t0.500000\n"
+    for i in range(600):
+        with open(os.path.join(tmp_path, "s%04d.vaf" % i), "w") as f:
+            f.write("#header\n" + "".join(row % (j, j) for j in range(3)))
+    p = subprocess.run([sys.executable, "-c", _MANY_FILES, PKG, str(tmp_path), "600", str(threads)],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "ok 600" in p.stdout, p.stderr[-2000:]
+
+
 # --- GPU ---------------------------------------------------------------------
 
 @pytest.mark.gpu

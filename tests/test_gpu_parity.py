@@ -437,6 +437,87 @@ def test_full_size_linearity_and_prefix_parity(torch_dev, config):
     m.close()
 
 
+def test_c4_full_size_sharded(torch_dev):
+    """C4 at its full size on one GPU: 1B x 150 bp reads HBM-resident (162 GB of
+    288).  Counted once by a single-shard counter and once through
+    vc_create_multi(devices=[0, 0]) -- the two halves dealt to the two shards by
+    vc_count_device, summed on the device by vc_finish -- the totals are equal
+    (linearity: all = first half + second half, mod 2^32), the k-mer tallies add
+    up, and an exact 1M-read prefix matches the oracle.  The reference counts
+    every block of every file into one set of u32 counters
+    (vaf-counter.c:473-477,647-650); sharding must not change them."""
+    import torch
+    import vafc
+    import vafc_synth as S
+    import oracle as O
+    import tempfile
+    torch.cuda.empty_cache()
+    R, L, k = 1_000_000_000, 150, 21
+    panel = S.grch38_panel()
+    d_seq = torch.empty(R * L, dtype=torch.uint8, device=torch_dev)
+    d_offs = torch.empty(R, dtype=torch.int64, device=torch_dev)
+    d_lens = torch.empty(R, dtype=torch.int32, device=torch_dev)
+    win = torch.from_numpy(panel.windows().reshape(-1)).to(torch_dev)
+    dos = torch.from_numpy(panel.dosage.astype(np.uint8)).to(torch_dev)
+    torch.cuda.synchronize()
+    vafc.synth_reads(d_seq.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), 0, R, L, 42, 0.01,
+                     win.data_ptr(), dos.data_ptr(), panel.n, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    with tempfile.TemporaryDirectory() as d:
+        pat = os.path.join(d, "p.txt")
+        panel.write_patterns(pat, k)
+        db = vafc.load_patterns(pat)
+        keys, vals, _ = db.keys(k)
+        orc = O.Oracle(k, pattern_fn=pat)
+    one = vafc.KmerMap(k, keys, vals, db.n, 0)
+    one.count_device(d_seq.data_ptr(), R * L, d_offs.data_ptr(), d_lens.data_ptr(), R)
+    all_c, all_k = one.finish()
+    two = vafc.KmerMap(k, keys, vals, db.n, devices=[0, 0])
+    h = R // 2
+    two.count_device(d_seq.data_ptr(), R * L, d_offs.data_ptr(), d_lens.data_ptr(), h)
+    two.count_device(d_seq.data_ptr(), R * L, d_offs.data_ptr() + 8 * h, d_lens.data_ptr() + 4 * h, R - h)
+    assert [b for _, b in two.shards()] == [1, 1]
+    sh_c, sh_k = two.finish()
+    assert sh_k == all_k and np.array_equal(sh_c, all_c)
+    # the halves on their own add up to the whole
+    one.reset()
+    one.count_device(d_seq.data_ptr(), R * L, d_offs.data_ptr(), d_lens.data_ptr(), h)
+    a_c, a_k = one.finish()
+    one.reset()
+    one.count_device(d_seq.data_ptr(), R * L, d_offs.data_ptr() + 8 * h, d_lens.data_ptr() + 4 * h, R - h)
+    b_c, b_k = one.finish()
+    assert all_k == a_k + b_k
+    assert np.array_equal(all_c, (a_c.astype(np.uint64) + b_c).astype(np.uint32))
+    assert all_k > R * (L - k - 10)
+    assert int(all_c.astype(np.uint64).sum()) > R // 200
+    n = 1_000_000
+    one.reset()
+    one.count_device(d_seq.data_ptr(), n * L, d_offs.data_ptr(), d_lens.data_ptr(), n)
+    p_c, p_k = one.finish()
+    seq = d_seq[: n * L].cpu().numpy()
+    want, km_want = orc.count_reads(seq, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint32))
+    assert p_k == km_want and np.array_equal(p_c, want)
+    one.close()
+    two.close()
+    del d_seq, d_offs, d_lens
+    torch.cuda.empty_cache()
+
+
+def test_short_reads_whole_wave(torch_dev):
+    """Waves whose reads all fit in one 16-base chunk (lengths 0..16, below k):
+    the quad scan's peeled chunk 0 is the whole span; nothing is counted
+    twice, and mixed waves with longer reads still match the oracle."""
+    rng = np.random.default_rng(44)
+    for k in (21, 31):
+        short = random_reads(rng, list(rng.integers(0, 17, 4096)))
+        mixed = random_reads(rng, list(rng.integers(0, 17, 2000)) + [150] * 64 + list(rng.integers(0, 40, 2000)))
+        for reads in (short, mixed):
+            keys, vals, n_pat = table_from_reads(k, reads + random_reads(rng, [200] * 20), rng, n_pat=300)
+            want, km_want = oracle_counts(k, keys, vals, n_pat, reads)
+            got, km = gpu_counts(k, keys, vals, n_pat, reads)
+            assert km == km_want and np.array_equal(got, want)
+
+
 def test_bound_outputs_accumulate_and_wrap(torch_dev):
     """Counts bound to a caller buffer accumulate modulo 2^32 (uint32 semantics)."""
     import torch

@@ -7,7 +7,7 @@
 #   tools/asan_tests.sh [pytest args...]     (CPU only; no GPU needed)
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-make -s -j8 -C "$ROOT/kmer-cnt_amd/csrc" asan=1 ../lib_asan/libvafc.so
+make -s -j8 -C "$ROOT/kmer-cnt_amd/csrc" asan=1 ../lib_asan/libvafc.so ../lib_asan/vaf-counter
 make -s -j8 -C "$ROOT/oracle"
 RT=$(/opt/rocm/llvm/bin/clang++ -print-file-name=libclang_rt.asan-x86_64.so)
 cd "$ROOT"
