@@ -52,3 +52,28 @@ def test_cli_run_parses_reference_speed_line(tmp_path):
     S.write_fastq(fq, panel, 2000, f_snp=0.5)
     r = bench.cli_run(bench.REF_CLI, pat, fq, 1, str(tmp_path / "o.vaf"), 21)
     assert r["bases"] == 2000 * 150 and r["mbases"] > 0 and r["mkmers"] > 0
+
+
+def test_fastq_bytes_np_equals_fastq_bytes():
+    """The array-built FASTQ records of the end-to-end file are the bytes of the
+    per-record writer the goldens use, across read-number digit boundaries."""
+    import vafc_synth as S
+    rng = np.random.default_rng(3)
+    reads = np.frombuffer(b"ACGTN", np.uint8)[rng.integers(0, 5, (3000, 150))]
+    for first in (0, 7, 98, 997, 9_999_000, 99_999_999 - 1500):
+        assert S.fastq_bytes_np(reads, first) == S.fastq_bytes(reads, first), first
+
+
+def test_vaf_counts_reads_the_writer_output(tmp_path):
+    """bench.vaf_counts parses the .vaf writer's counts back (the N > 1 parity
+    compares all-reduced counts with N x the reference's)."""
+    import bench
+    import vafc
+    import vafc_synth as S
+    panel = S.make_panel(S.synthetic_bed(50))
+    pat = str(tmp_path / "p.txt")
+    panel.write_patterns(pat, 21)
+    db = vafc.load_patterns(pat)
+    counts = np.random.default_rng(1).integers(0, 2 ** 32, 2 * db.n, dtype=np.uint64).astype(np.uint32)
+    db.write_vaf(counts, str(tmp_path / "o.vaf"))
+    assert np.array_equal(bench.vaf_counts(str(tmp_path / "o.vaf")), counts)
