@@ -39,6 +39,19 @@
 
 #define WAVE 64
 
+// Build-time A/B knobs (make XFLAGS=...; tools/ab_libs.sh): the round-2 forms
+// of two parts of the flank kernels, kept for comparison.
+#ifdef VC_FLANK_WORD
+#define VC_FLANK_U8 0          // flank lookups: 32-bit words, per-base extraction
+#else
+#define VC_FLANK_U8 1          // flank lookups: bytes, two v_bfe_u32 of one register
+#endif
+#ifdef VC_FWD_ONLY
+#define VC_SCAN_FB 0           // every lane scans forwards
+#else
+#define VC_SCAN_FB 1           // odd lanes scan backwards (scan_span_quad_fb)
+#endif
+
 // ---------------------------------------------------------------------------
 // small helpers
 // ---------------------------------------------------------------------------
@@ -542,6 +555,42 @@ __device__ __forceinline__ int clamp16(int v) { return v < 0 ? 0 : (v > 16 ? 16 
 // in the bitmap -- word bits 5..19, bit bits 0..4 (v_bfe_u32 uses the low 5
 // bits of its offset).  5 VALU per base: extraction, shift, mask, test, merge.
 // Bases j < J0 or j >= J1 are not looked up (their bits stay 0).
+//
+// Byte form (the default; -DVC_FLANK_WORD = the word form below): the bitmap
+// is the same bytes read one byte at a time, byte v >> 3, bit v & 7.  The
+// byte address (bits 3..19 of the 10-mer) and the bit index (bits 0..2) are
+// two v_bfe_u32 of ONE register that holds the whole 10-mer: Bc for bases
+// 9..15, M7 = bases -8..7 for bases 1..7, M8 = bases -7..8 for base 8 and
+// M0 = bases -15..0 for base 0 (three v_alignbit per chunk).  4 VALU per base
+// plus 3 per chunk, against 5 per base: no per-base extraction, and no mask
+// (the byte address needs none; the 32-bit word address needed shift + mask).
+template <int J0, int J1, int ABL = 0>
+__device__ __forceinline__ uint32_t flank_bits_u8(uint32_t Bm1, uint32_t Bc)
+{
+	typedef const uint8_t __attribute__((address_space(3))) lds_u8_t;
+	const uint32_t M7 = J0 <= 7 && J1 > 1 ? __builtin_amdgcn_alignbit(Bm1, Bc, 16u) : 0u;
+	const uint32_t M8 = J0 <= 8 && J1 > 8 ? __builtin_amdgcn_alignbit(Bm1, Bc, 14u) : 0u;
+	const uint32_t M0 = J0 == 0 ? __builtin_amdgcn_alignbit(Bm1, Bc, 30u) : 0u;
+	uint32_t fb[16], fi[16];
+#pragma unroll
+	for (int j = J0; j < J1; ++j) {
+		const uint32_t src = j >= 9 ? Bc : (j == 8 ? M8 : (j >= 1 ? M7 : M0));
+		const uint32_t s = j >= 9 ? 2u * (15 - j) : (j == 8 || j == 0 ? 0u : 2u * (7 - j));
+		const uint32_t a = __builtin_amdgcn_ubfe(src, s + 3u, 2 * VC_FLANK_BASES - 3);
+		fi[j] = __builtin_amdgcn_ubfe(src, s, 3u);
+		if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(a)); fb[j] = a; }
+		else fb[j] = *(lds_u8_t *)(uintptr_t)a;   // the filter sits at LDS address 0
+	}
+	uint32_t R0 = 0, R1 = 0;
+#pragma unroll
+	for (int j = J0; j < J1; ++j) {
+		const uint32_t t = __builtin_amdgcn_ubfe(fb[j], fi[j], 1u);
+		uint32_t &R = (j & 1) ? R1 : R0;
+		asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(R) : "v"(t), "i"(15 - j), "v"(R));
+	}
+	return R0 | R1;
+}
+
 template <int J0, int J1, int ABL = 0>
 __device__ __forceinline__ uint32_t flank_bits(uint32_t fbase, uint32_t Bm1, uint32_t Bc)
 {
@@ -602,7 +651,8 @@ __device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, i
 		// there; window j passes iff the 10-mers ending at j (its last ten
 		// bases) and at j - (K - 10) (its first ten) are both in the set
 		(void)fsh; (void)wmask4; (void)Cm2;
-		hm = flank_bits<J0, J1, ABL>(fbase, Bm1, Bc);
+		if constexpr (VC_FLANK_U8) hm = flank_bits_u8<J0, J1, ABL>(Bm1, Bc);
+		else hm = flank_bits<J0, J1, ABL>(fbase, Bm1, Bc);
 		const uint32_t P = (H << 16) | hm;           // R of chunks c-1 | c, c-2 in H >> 16
 		hm &= __builtin_amdgcn_alignbit(H >> 16, P, (uint32_t)(K - VC_FLANK_BASES));
 		H = P;
@@ -714,7 +764,7 @@ __device__ __forceinline__ void hit_loop2(const VcKernelArgs &A, WaveQueue &Q, u
 // the windows that span it) and the stream rotation of packed_chunk, without
 // its 16 filter lookups, validity mask, tally or hit loop.
 template <int K, int ABL>
-__device__ __forceinline__ void packed_streams(int c, int tail_c, int nt4m, uint32_t sh, uint32_t w0, uint32_t w1,
+__device__ __forceinline__ void packed_streams(const VcKernelArgs &A, int c, int tail_c, int nt4m, uint32_t sh, uint32_t w0, uint32_t w1,
                                                uint32_t w2, uint32_t w3, uint32_t w4, uint32_t &Bm1, uint32_t &Bm2,
                                                uint32_t &Cm1, uint32_t &Cm2, int &U, int &Qe, uint32_t &H,
                                                const uint32_t *__restrict__ filt)
@@ -749,7 +799,8 @@ __device__ __forceinline__ void packed_streams(int c, int tail_c, int nt4m, uint
 		// the first window (ending at K - 1) starts with the 10-mer ending at
 		// base 9: chunk 0's bases 9..15 are looked up for the later windows
 		static_assert(K - VC_FLANK_BASES >= 9, "flank mode needs the first window's head in chunk 0");
-		H = flank_bits<VC_FLANK_BASES - 1, 16, ABL>(lds_base(filt), Bm1, Bc);
+		if constexpr (VC_FLANK_U8) H = flank_bits_u8<VC_FLANK_BASES - 1, 16, ABL>(Bm1, Bc);
+		else H = flank_bits<VC_FLANK_BASES - 1, 16, ABL>(lds_base(filt), Bm1, Bc);
 	}
 	Bm2 = Bm1; Bm1 = Bc;
 	Cm2 = Cm1; Cm1 = ~L;
@@ -853,7 +904,7 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	if constexpr (PEEL) {
 		if (nit > 0 && (A.variant & 1u) == 0) {
 			quad_fix(d1, w1, w2, w3, w4);
-			packed_streams<K, ABL>(c_lo, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt);
+			packed_streams<K, ABL>(A, c_lo, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt);
 			w0 = w4; w1 = w5; w2 = w6; w3 = w7; w4 = w8; d1 = d5;
 			w5 = x5; w6 = x6; w7 = x7; w8 = x8; d5 = d9;
 			wi += 4;
@@ -969,7 +1020,7 @@ __device__ __forceinline__ void scan_span_quad(const VcKernelArgs &A, const uint
 	if constexpr (PEEL) {
 		if ((A.variant & 1u) == 0) {
 			quad_fix(d[0], w[1], w[2], w[3], w[4]);
-			packed_streams<K, ABL>(c_lo, tail_c, nt4m, sh, w[0], w[1], w[2], w[3], w[4], Bm1, Bm2, Cm1, Cm2, U, Qe, H,
+			packed_streams<K, ABL>(A, c_lo, tail_c, nt4m, sh, w[0], w[1], w[2], w[3], w[4], Bm1, Bm2, Cm1, Cm2, U, Qe, H,
 			                       filt);
 #pragma unroll
 			for (int i = 0; i < 13; ++i) w[i] = w[i + 4];
@@ -1060,6 +1111,343 @@ __device__ __forceinline__ void scan_span_quad(const VcKernelArgs &A, const uint
 		chunk(J0Tag<0>{}, J0Tag<16>{}, cl, 0);
 }
 
+// ---------------------------------------------------------------------------
+// flank kernels, whole reads: odd lanes scan their read backwards
+// ---------------------------------------------------------------------------
+//
+// Lane r reads read r, and read r's last bytes share a 128-byte line with
+// read r + 1's first bytes.  Scanned forwards by both lanes, that line is
+// fetched by lane r + 1 at its first trip and by lane r at its last, about
+// 15 us apart, and the L2 has usually dropped it in between (HBM traffic
+// 1.6x the read bytes).  Here odd lanes scan the reverse complement of their
+// read, last chunk first: lane 2i + 1 starts at the line it shares with lane
+// 2i + 2 and ends at the one it shares with lane 2i, so each shared line is
+// requested by both lanes in the same load instruction.
+//
+// A backward lane's chunk c' is read bytes [len - 16c' - 16, len - 16c') of
+// its read, complemented and reversed.  The canonical k-mers, the window
+// validity (in reverse-complement coordinates [0, len)), the tally and the
+// flank test (the bitmap is closed under reverse complement) are unchanged;
+// the queued k-mers are the reverse complements, canonicalised by the drain.
+//
+// Registers: quad q of a window holds the chunk's first four dwords in
+// address order for both directions, w[0] the fifth dword of the window's
+// first chunk (forwards: the dword after, backwards: the dword after, too --
+// which for a backward lane is the first dword of the chunk scanned before).
+// The four realigned dwords in quad order are q0..q3; forwards they are the
+// chunk's bytes 0..15, backwards bytes 12..15, 0..3, 4..7, 8..11 (q1..q3 are
+// the same v_alignbyte for both).  Packing then differs only in per-lane
+// constants: the multiplier (codes reversed inside a byte, or not), one perm
+// selector and the complement (Dir).  Cost: 2 v_cndmask per chunk.
+
+struct Dir {
+	bool bwd;
+	uint32_t mul;     // 0x40100401: a byte's codes reversed (forwards); 0x01041040: in order (backwards)
+	uint32_t sel13;   // perm selector placing dwords q1 and q3
+	uint32_t inv;     // 0 forwards, ~0 backwards (the complement)
+};
+
+// Byte mask of the bytes i >= e of a dword (e <= 0: all, e >= 4: none).
+__device__ __forceinline__ uint32_t bytes_from(int e)
+{
+	return e <= 0 ? 0xFFFFFFFFu : (e >= 4 ? 0u : (0xFFFFFFFFu << (8 * e)));
+}
+
+// Decode of a chunk's four realigned dwords (quad order) with the read's
+// tail rule (vaf-counter.c:261-291): forwards the tail chunk decodes with
+// seq_nt4_table throughout; backwards chunk 0 holds the read's last 16
+// bytes, of which the last len % 16 (its first bytes in scan order:
+// tail_e = 16 - len % 16 in read order) are the tail.
+__device__ __forceinline__ void dec_chunk_fb(const Dir &D, int c, int tail_c, int nt4m, int tail_e, uint32_t q0,
+                                             uint32_t q1, uint32_t q2, uint32_t q3, uint32_t &t0, uint32_t &t1,
+                                             uint32_t &t2, uint32_t &t3)
+{
+	t0 = dec_code(q0); t1 = dec_code(q1); t2 = dec_code(q2); t3 = dec_code(q3);
+	const int cm = c | nt4m;
+	if (__ballot(cm == tail_c)) {
+		if (cm == tail_c) {
+			// read-order dword of q_m: forwards m, backwards (m + 3) & 3
+			const int e = D.bwd ? tail_e : -64;
+			uint32_t mk = bytes_from(e - 12);
+			t0 = (dec_tail(q0) & mk) | (t0 & ~mk);
+			mk = bytes_from(e);
+			t1 = (dec_tail(q1) & mk) | (t1 & ~mk);
+			mk = bytes_from(e - 4);
+			t2 = (dec_tail(q2) & mk) | (t2 & ~mk);
+			mk = bytes_from(e - 8);
+			t3 = (dec_tail(q3) & mk) | (t3 & ~mk);
+		}
+	}
+}
+
+// The chunk's big-endian stream in scan order (see Dir).
+__device__ __forceinline__ uint32_t pack_fb(const Dir &D, uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3)
+{
+	const uint32_t g0 = (t0 & 0x03030303u) * D.mul;
+	const uint32_t g1 = (t1 & 0x03030303u) * D.mul;
+	const uint32_t g2 = (t2 & 0x03030303u) * D.mul;
+	const uint32_t g3 = (t3 & 0x03030303u) * D.mul;
+	const uint32_t p13 = __builtin_amdgcn_perm(g1, g3, D.sel13);
+	const uint32_t p02 = __builtin_amdgcn_perm(g0, g2, 0x070C030Cu);   // byte 1: q2, byte 3: q0
+	return (p13 | p02) ^ D.inv;
+}
+
+// Invalid bases of the chunk, base j (scan order) at bit 2j; slow path.
+__device__ __forceinline__ uint32_t invalid_bits_fb(const Dir &D, uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3,
+                                                    uint32_t q0, uint32_t q1, uint32_t q2, uint32_t q3)
+{
+	t0 |= dec_bit3(q0); t1 |= dec_bit3(q1); t2 |= dec_bit3(q2); t3 |= dec_bit3(q3);
+	const uint32_t Im = ((t0 >> 2) & 0x01010101u) | (t1 & 0x04040404u) |
+	                    ((t2 << 2) & 0x10101010u) | ((t3 << 4) & 0x40404040u);
+	const uint32_t F = transpose2x4x4(Im);     // quad-order byte p at bit 2p
+	// backwards: quad order -> read order (rotate by one dword), then reverse
+	return D.bwd ? pairrev(__builtin_amdgcn_alignbit(F, F, 8u)) : F;
+}
+
+template <int K, int ABL, int J0 = 0, int J1 = 16, bool DEFER = false>
+__device__ __forceinline__ uint32_t packed_chunk_fb(const VcKernelArgs &A, const Dir &D, int c, int tail_c, int nt4m,
+                                                    int tail_e, uint32_t q0, uint32_t q1, uint32_t q2, uint32_t q3,
+                                                    uint32_t &Bm1, uint32_t &Bm2, int &U, int &Qe, uint32_t &H,
+                                                    const uint32_t *__restrict__ filt, WaveQueue &Q, uint32_t &tl,
+                                                    int lane)
+{
+	constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
+	uint32_t t0, t1, t2, t3;
+	dec_chunk_fb(D, c, tail_c, nt4m, tail_e, q0, q1, q2, q3, t0, t1, t2, t3);
+	U += 16;
+	Qe += 16;
+	const uint32_t Bc = pack_fb(D, t0, t1, t2, t3);
+	uint32_t hm;
+	if constexpr (VC_FLANK_U8) hm = flank_bits_u8<J0, J1, ABL>(Bm1, Bc);
+	else hm = flank_bits<J0, J1, ABL>(lds_base(filt), Bm1, Bc);
+	const uint32_t P = (H << 16) | hm;
+	hm &= __builtin_amdgcn_alignbit(H >> 16, P, (uint32_t)(K - VC_FLANK_BASES));
+	H = P;
+	uint32_t V = ((1u << clamp16(U)) - 1u) & ~((1u << clamp16(Qe)) - 1u);
+	const uint32_t anyinv = ((t0 | t1 | t2 | t3) & 0x04040404u) | ((q0 | q1 | q2 | q3) & 0x08080808u);
+	if (__ballot(anyinv != 0u)) {
+		if (anyinv != 0u) {
+			const uint32_t F = invalid_bits_fb(D, t0, t1, t2, t3, q0, q1, q2, q3);
+			const int j0 = (int)((uint32_t)__builtin_ctz(F) >> 1);
+			const int j1 = (int)((31u - (uint32_t)__builtin_clz(F)) >> 1);
+			V &= ~((2u << (15 - j0)) - 1u);
+			const int u1 = 16 - j1 - K;
+			U = U < u1 ? U : u1;
+		}
+	}
+	hm &= V;
+	tl += (uint32_t)__builtin_popcount(V);
+	if constexpr (DEFER) {
+		Bm2 = Bm1; Bm1 = Bc;
+		return hm;
+	} else if constexpr ((ABL & 4) != 0) {
+		asm volatile("" :: "v"(hm));
+	} else if (__ballot(hm != 0u)) {
+		for (;;) {
+			const bool has = hm != 0u;
+			const uint64_t bal = __ballot(has);
+			if (!bal) break;
+			const uint32_t b = (uint32_t)__builtin_ctz(hm | 0x80000000u);
+			const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, 2u * b);
+			const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
+			queue_append(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
+			hm &= hm - 1u;
+		}
+	}
+	Bm2 = Bm1; Bm1 = Bc;
+	return 0u;
+}
+
+// Chunk 0 of a whole read (no window can end in it, K >= 17): streams only.
+template <int K, int ABL>
+__device__ __forceinline__ void packed_streams_fb(const VcKernelArgs &A, const Dir &D, int c, int tail_c, int nt4m,
+                                                  int tail_e, uint32_t q0, uint32_t q1, uint32_t q2, uint32_t q3,
+                                                  uint32_t &Bm1, uint32_t &Bm2, int &U, int &Qe, uint32_t &H)
+{
+	uint32_t t0, t1, t2, t3;
+	dec_chunk_fb(D, c, tail_c, nt4m, tail_e, q0, q1, q2, q3, t0, t1, t2, t3);
+	U += 16;
+	Qe += 16;
+	const uint32_t anyinv = ((t0 | t1 | t2 | t3) & 0x04040404u) | ((q0 | q1 | q2 | q3) & 0x08080808u);
+	if (__ballot(anyinv != 0u)) {
+		if (anyinv != 0u) {
+			const uint32_t F = invalid_bits_fb(D, t0, t1, t2, t3, q0, q1, q2, q3);
+			const int j1 = (int)((31u - (uint32_t)__builtin_clz(F)) >> 1);
+			const int u1 = 16 - j1 - K;
+			U = U < u1 ? U : u1;
+		}
+	}
+	const uint32_t Bc = pack_fb(D, t0, t1, t2, t3);
+	static_assert(K - VC_FLANK_BASES >= 9, "flank mode needs the first window's head in chunk 0");
+	if constexpr (VC_FLANK_U8) H = flank_bits_u8<VC_FLANK_BASES - 1, 16, ABL>(Bm1, Bc);
+	else H = flank_bits<VC_FLANK_BASES - 1, 16, ABL>(0u, Bm1, Bc);
+	Bm2 = Bm1; Bm1 = Bc;
+}
+
+// A quad of dwords [q, q + 4) loaded from inside [0, wmax]: a quad that would
+// leave the buffer is loaded from its nearest end and the return value says
+// how far it was moved (positive: back from the end, negative: up from the
+// start); quad_fix_fb shifts the dwords into place.  Dwords outside the
+// buffer are never part of a read.
+__device__ __forceinline__ int ldq_fb(const uint32_t *__restrict__ s32, int64_t q, uint64_t wmax,
+                                      uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
+{
+	const int64_t lim = (int64_t)wmax - 3;
+	const int64_t cq = q < 0 ? 0 : (q > lim ? lim : q);
+	const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(s32 + cq);
+	a = v.x; b = v.y; c = v.z; d = v.w;
+	const int64_t sft = q - cq;
+	return sft > 3 ? 3 : (sft < -3 ? -3 : (int)sft);
+}
+
+template <bool SAFE>
+__device__ __forceinline__ int ldq_fb_s(const uint32_t *__restrict__ s32, int64_t q, uint64_t wmax,
+                                        uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
+{
+	if constexpr (SAFE) {
+		const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(s32 + q);
+		a = v.x; b = v.y; c = v.z; d = v.w;
+		return 0;
+	} else {
+		return ldq_fb(s32, q, wmax, a, b, c, d);
+	}
+}
+
+__device__ __forceinline__ void quad_fix_fb(int sft, uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
+{
+	if (__ballot(sft != 0)) {        // only the reads at either end of the buffer
+		asm volatile("");
+		// new[s] = old[s + sft] where 0 <= s + sft <= 3 (the rest is outside the buffer)
+		const uint32_t a0 = a, b0 = b, c0 = c, d0 = d;
+		a = sft == 1 ? b0 : (sft == 2 ? c0 : (sft == 3 ? d0 : a0));
+		b = sft == 1 ? c0 : (sft >= 2 ? d0 : (sft == -1 ? a0 : b0));
+		c = sft == 1 ? d0 : (sft == -1 ? b0 : (sft <= -2 ? a0 : c0));
+		d = sft == -1 ? c0 : (sft == -2 ? b0 : (sft == -3 ? a0 : d0));
+	}
+}
+
+template <int K, int ABL = 0, bool SAFE = false>
+__device__ __forceinline__ void scan_span_quad_fb(const VcKernelArgs &A, const uint32_t *__restrict__ s32,
+                                                  uint64_t wmax, uint64_t off, int len, int nit,
+                                                  const uint32_t *__restrict__ filt, WaveQueue &Q, uint32_t &tl,
+                                                  int lane)
+{
+	static_assert(K >= VC_FLANK_MIN_K, "flank kernels only");
+	if (nit == 0) return;
+	Dir D;
+	D.bwd = (lane & 1) != 0 && (A.variant & 256u) == 0;   // A.variant bit 8: all lanes forwards (A/B)
+	D.mul = D.bwd ? 0x01041040u : 0x40100401u;
+	D.sel13 = D.bwd ? 0x0C030C07u : 0x0C070C03u;
+	D.inv = D.bwd ? 0xFFFFFFFFu : 0u;
+	const int nt4m = -(int)A.nt4;
+	const int tail_c = A.nt4 ? -1 : ((len & 15) ? (D.bwd ? 0 : (len >> 4)) : -1);
+	const int tail_e = 16 - (len & 15);
+	// forwards: chunk c at read bytes 16c..; backwards at len - 16c - 16..
+	const int64_t a0 = D.bwd ? (int64_t)off + len - 16 : (int64_t)off;
+	const int64_t x0 = a0 >> 2;                                      // floor, also below 0
+	const uint32_t sh = (uint32_t)(a0 & 3);
+	const int64_t qs = D.bwd ? -4 : 4;                               // dwords per chunk, signed
+	int64_t qb = D.bwd ? x0 : x0 + 1;                                // quad of the window's first chunk
+	uint32_t w[17];
+	int d[4];
+	{
+		const int64_t w0i = D.bwd ? x0 + 4 : x0;
+		const int64_t w0c = w0i < 0 ? 0 : ((uint64_t)w0i > wmax ? (int64_t)wmax : w0i);
+		w[0] = s32[SAFE ? w0i : w0c];
+	}
+#pragma unroll
+	for (int q = 0; q < 4; ++q)
+		d[q] = ldq_fb_s<SAFE>(s32, qb + q * qs, wmax, w[4 * q + 1], w[4 * q + 2], w[4 * q + 3], w[4 * q + 4]);
+	uint32_t x0_ = 0, x1 = 0, x2 = 0, x3 = 0;
+	int dx = ldq_fb_s<SAFE>(s32, qb + 4 * qs, wmax, x0_, x1, x2, x3);
+
+	uint32_t Bm1 = 0, Bm2 = 0, H = 0;
+	int U = 1 - K;
+	int Qe = -len;
+	// realigned dwords of window chunk i (quad order)
+	auto quads = [&](int i, uint32_t &q0, uint32_t &q1, uint32_t &q2, uint32_t &q3) {
+		const uint32_t G = D.bwd ? (i == 0 ? w[0] : w[4 * i - 3]) : w[4 * i + 1];
+		const uint32_t Hh = D.bwd ? w[4 * i + 4] : w[4 * i];
+		q0 = __builtin_amdgcn_alignbyte(G, Hh, sh);
+		q1 = __builtin_amdgcn_alignbyte(w[4 * i + 2], w[4 * i + 1], sh);
+		q2 = __builtin_amdgcn_alignbyte(w[4 * i + 3], w[4 * i + 2], sh);
+		q3 = __builtin_amdgcn_alignbyte(w[4 * i + 4], w[4 * i + 3], sh);
+	};
+	// chunk 0 builds only the streams
+	{
+		quad_fix_fb(d[0], w[1], w[2], w[3], w[4]);
+		uint32_t q0, q1, q2, q3;
+		quads(0, q0, q1, q2, q3);
+		packed_streams_fb<K, ABL>(A, D, 0, tail_c, nt4m, tail_e, q0, q1, q2, q3, Bm1, Bm2, U, Qe, H);
+		const uint32_t e1 = D.bwd ? w[1] : w[4];                    // the fifth dword of chunk 1
+#pragma unroll
+		for (int i = 1; i < 13; ++i) w[i] = w[i + 4];
+		w[0] = e1;
+		w[13] = x0_; w[14] = x1; w[15] = x2; w[16] = x3;
+		d[0] = d[1]; d[1] = d[2]; d[2] = d[3]; d[3] = dx;
+		qb += qs;
+	}
+	if (nit == 1) return;            // wave-uniform
+	int it = 1;
+	auto chunk = [&](auto j1tag, int c, int i) {
+		uint32_t q0, q1, q2, q3;
+		quads(i, q0, q1, q2, q3);
+		packed_chunk_fb<K, ABL, 0, decltype(j1tag)::value>(A, D, c, tail_c, nt4m, tail_e, q0, q1, q2, q3, Bm1, Bm2,
+		                                                    U, Qe, H, filt, Q, tl, lane);
+	};
+	auto dchunk = [&](int c, int i) -> uint32_t {
+		uint32_t q0, q1, q2, q3;
+		quads(i, q0, q1, q2, q3);
+		return packed_chunk_fb<K, ABL, 0, 16, true>(A, D, c, tail_c, nt4m, tail_e, q0, q1, q2, q3, Bm1, Bm2, U, Qe,
+		                                            H, filt, Q, tl, lane);
+	};
+	for (; it + 4 < nit; it += 4) {
+		uint32_t n[16];
+		int dn[4];
+#pragma unroll
+		for (int q = 0; q < 4; ++q)
+			dn[q] = ldq_fb_s<SAFE>(s32, qb + (4 + q) * qs, wmax, n[4 * q], n[4 * q + 1], n[4 * q + 2], n[4 * q + 3]);
+#pragma unroll
+		for (int q = 0; q < 4; ++q) quad_fix_fb(d[q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3], w[4 * q + 4]);
+#pragma unroll
+		for (int p = 0; p < 2; ++p) {
+			const uint32_t s2 = Bm2, s1 = Bm1;
+			uint32_t h = dchunk(it + 2 * p, 2 * p);
+			h = (h << 16) | dchunk(it + 2 * p + 1, 2 * p + 1);
+			hit_loop2<K, ABL>(A, Q, h, s2, s1, Bm2, Bm1, lane);
+		}
+		w[0] = D.bwd ? w[13] : w[16];
+#pragma unroll
+		for (int i = 0; i < 16; ++i) w[i + 1] = n[i];
+#pragma unroll
+		for (int q = 0; q < 4; ++q) d[q] = dn[q];
+		qb += 4 * qs;
+	}
+	// the last 1..4 chunks, all in w already (wave-uniform count)
+#pragma unroll
+	for (int q = 0; q < 4; ++q) quad_fix_fb(d[q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3], w[4 * q + 4]);
+	const int r = nit - it;
+	if (r >= 2) chunk(J0Tag<16>{}, it, 0);
+	if (r >= 3) chunk(J0Tag<16>{}, it + 1, 1);
+	if (r >= 4) chunk(J0Tag<16>{}, it + 2, 2);
+	// the wave's last chunk (window chunk r - 1): only its lower 8 windows when
+	// no lane has more valid ones (see scan_span_packed)
+	const int i = r - 1;
+	if (i != 0) {
+		const uint32_t e = D.bwd ? (i == 1 ? w[1] : (i == 2 ? w[5] : w[9])) : (i == 1 ? w[4] : (i == 2 ? w[8] : w[12]));
+		w[1] = i == 1 ? w[5] : (i == 2 ? w[9] : w[13]);
+		w[2] = i == 1 ? w[6] : (i == 2 ? w[10] : w[14]);
+		w[3] = i == 1 ? w[7] : (i == 2 ? w[11] : w[15]);
+		w[4] = i == 1 ? w[8] : (i == 2 ? w[12] : w[16]);
+		w[0] = e;
+	}
+	const int cl = nit - 1;
+	if ((A.variant & 4u) == 0 && __ballot(len - 16 * cl > 8) == 0)
+		chunk(J0Tag<8>{}, cl, 0);
+	else
+		chunk(J0Tag<16>{}, cl, 0);
+}
+
 // k in 16..31 with a compile-time specialisation: packed streams (the quad
 // loop unless A.variant bit 3 or a memory ablation); otherwise the general
 // rolling scan.
@@ -1069,6 +1457,14 @@ __device__ __forceinline__ void scan_any(const VcKernelArgs &A, const uint32_t *
                                          int vlo, int vhi, int nit, const uint32_t *__restrict__ filt,
                                          WaveQueue &Q, uint32_t &tl, int lane)
 {
+	if constexpr (K >= VC_FLANK_MIN_K && (ABL & VC_KV_FLANK) != 0 && !HAS_LO && (ABL & (2 | 8 | 16 | 32)) == 0) {
+		// flank kernels, whole reads: odd lanes scan backwards (-DVC_FWD_ONLY:
+		// the forwards-only quad loop of round 2, for A/B)
+		if constexpr (VC_SCAN_FB) {
+			scan_span_quad_fb<K, ABL, SAFE>(A, s32, wmax, off, len, nit, filt, Q, tl, lane);
+			return;
+		}
+	}
 	if constexpr (K >= 16) {
 		if constexpr ((ABL & (2 | 8 | 16)) == 0) {
 #ifdef VC_ABLATION
@@ -1092,6 +1488,9 @@ __device__ __forceinline__ void load_filter(const VcKernelArgs &A, uint32_t *fil
 	uint4 *dst = reinterpret_cast<uint4 *>(filt);
 	for (uint32_t i = threadIdx.x; i < nw / 4u; i += blockDim.x) dst[i] = src[i];
 	if (threadIdx.x < 4) filt[nw + threadIdx.x] = 0u;     // the zero word(s)
+	// flank_bits_u8 addresses the filter from LDS address 0 (the kernels have
+	// no static LDS, so the dynamic array starts there; folds at compile time)
+	if (lds_base(filt) != 0u) __builtin_trap();
 	__syncthreads();
 }
 
@@ -1142,7 +1541,13 @@ vc_count_reads_kernel(VcKernelArgs A)
 		// the packed scan loads dwords [off/4, off/4 + 8 ceil(nit/2) + 13) (lanes
 		// past their span keep loading); groups clear of the buffer end skip the
 		// per-load clamping
-		const bool clear = (off >> 2) + 8u * (uint64_t)((nit + 1) >> 1) + 13u <= wmax;
+		bool clear = (off >> 2) + 8u * (uint64_t)((nit + 1) >> 1) + 13u <= wmax;
+		if constexpr ((ABL & VC_KV_FLANK) != 0) {
+			// backward lanes (scan_span_quad_fb) load dwords down to
+			// (off + len - 16) / 4 - 4 (nit + 2) and up to (off + len) / 4
+			const int64_t xb = ((int64_t)off + len - 16) >> 2;
+			clear = clear && xb - 4 * (int64_t)(nit + 6) >= 0 && (uint64_t)(xb + 4) <= wmax;
+		}
 		if (K >= 16 && __builtin_amdgcn_ballot_w64(!clear) == 0)
 			scan_any<K, false, ABL, true>(A, s32, wmax, off, len, 0, nch, 0, len, nit, filt, Q, tl, lane);
 		else
