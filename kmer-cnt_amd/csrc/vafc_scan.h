@@ -46,10 +46,10 @@
 #else
 #define VC_FLANK_U8 1          // flank lookups: bytes, two v_bfe_u32 of one register
 #endif
-#ifdef VC_FWD_ONLY
-#define VC_SCAN_FB 0           // every lane scans forwards
+#ifdef VC_SCAN_BWD
+#define VC_SCAN_FB 1           // odd lanes scan backwards (scan_span_quad_fb; measured slower)
 #else
-#define VC_SCAN_FB 1           // odd lanes scan backwards (scan_span_quad_fb)
+#define VC_SCAN_FB 0           // every lane scans forwards (the quad loop)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -1458,8 +1458,9 @@ __device__ __forceinline__ void scan_any(const VcKernelArgs &A, const uint32_t *
                                          WaveQueue &Q, uint32_t &tl, int lane)
 {
 	if constexpr (K >= VC_FLANK_MIN_K && (ABL & VC_KV_FLANK) != 0 && !HAS_LO && (ABL & (2 | 8 | 16 | 32)) == 0) {
-		// flank kernels, whole reads: odd lanes scan backwards (-DVC_FWD_ONLY:
-		// the forwards-only quad loop of round 2, for A/B)
+		// flank kernels, whole reads, -DVC_SCAN_BWD: odd lanes scan backwards
+		// (A/B only: same time as every lane forwards in the same code, and that
+		// code is 10 % slower than the quad loop)
 		if constexpr (VC_SCAN_FB) {
 			scan_span_quad_fb<K, ABL, SAFE>(A, s32, wmax, off, len, nit, filt, Q, tl, lane);
 			return;

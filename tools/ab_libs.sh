@@ -1,8 +1,8 @@
 #!/bin/bash
 # Build-time A/B variants of libvafc.so (tools only; never shipped):
 #   kmer-cnt_amd/lib_ab/<name>/libvafc.so built with XFLAGS, e.g.
-#   tools/ab_libs.sh fwd="-DVC_FWD_ONLY" r2="-DVC_FWD_ONLY -DVC_FLANK_WORD"
-# then on the GPU box: VAFC_LIB=kmer-cnt_amd/lib_ab/fwd/libvafc.so python tools/ab.py VAFC_VARIANT=0
+#   tools/ab_libs.sh fb="-DVC_SCAN_BWD" r2="-DVC_FLANK_WORD"
+# then on the GPU box: VAFC_LIB=kmer-cnt_amd/lib_ab/fb/libvafc.so python tools/ab.py VAFC_VARIANT=0
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 for spec in "$@"; do

@@ -6,7 +6,7 @@ set -e -o pipefail
 OUT=${1:?out}
 shift
 for rep in 1 2; do
-  for v in default fwd r2; do
+  for v in default fb r2; do
     if [ "$v" = default ]; then L=kmer-cnt_amd/lib/libvafc.so; else L=kmer-cnt_amd/lib_ab/$v/libvafc.so; fi
     echo "== $v (rep $rep)" >> "$OUT"
     if [ "$v" = default ]; then
