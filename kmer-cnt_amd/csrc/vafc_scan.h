@@ -548,6 +548,27 @@ __device__ __forceinline__ uint32_t pack_codes_rev(uint32_t t0, uint32_t t1, uin
 	return lo | hi;
 }
 
+// Invalid-base flags of a chunk, base j at bit 2j (the layout of pack_codes):
+// byte r of dword m is invalid if its LUT code has bit 2 set or its raw byte
+// has bit 3 set.  One multiply gathers a dword's four flags (bit 2 of each
+// byte, at 8r + 2) into its top byte: the terms 2^4, 2^10, 2^16, 2^22 put flag
+// r at 24 + 2r and every other partial product at a distinct position below
+// bit 24, so nothing carries; pack_codes' perms join the four top bytes.  15
+// VALU against 23 for a mask-and-shift gather plus a 4x4 2-bit transpose; it
+// runs on the invalid-base path, which a wave takes for 64 % of its chunks at
+// 0.1 % N (one N among 1,024 bases).
+__device__ __forceinline__ uint32_t invalid_flags(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3, uint32_t b0,
+                                                  uint32_t b1, uint32_t b2, uint32_t b3)
+{
+	const uint32_t g0 = ((t0 | (b0 >> 1)) & 0x04040404u) * 0x00410410u;
+	const uint32_t g1 = ((t1 | (b1 >> 1)) & 0x04040404u) * 0x00410410u;
+	const uint32_t g2 = ((t2 | (b2 >> 1)) & 0x04040404u) * 0x00410410u;
+	const uint32_t g3 = ((t3 | (b3 >> 1)) & 0x04040404u) * 0x00410410u;
+	const uint32_t lo = __builtin_amdgcn_perm(g1, g0, 0x0C0C0703u);
+	const uint32_t hi = __builtin_amdgcn_perm(g3, g2, 0x07030C0Cu);
+	return lo | hi;
+}
+
 __device__ __forceinline__ int clamp16(int v) { return v < 0 ? 0 : (v > 16 ? 16 : v); }
 
 // Flank-bitmap lookups of one chunk (VC_KV_FLANK): R with bit 15 - j set iff
@@ -687,11 +708,8 @@ __device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, i
 	const uint32_t anyinv = ((t0 | t1 | t2 | t3) & 0x04040404u) | ((b0 | b1 | b2 | b3) & 0x08080808u);
 	if (__ballot(anyinv != 0u)) {
 		if (anyinv != 0u) {
-			t0 |= dec_bit3(b0); t1 |= dec_bit3(b1); t2 |= dec_bit3(b2); t3 |= dec_bit3(b3);
 			// invalid flags packed like the codes: base j at bit 2j of F
-			const uint32_t Im = ((t0 >> 2) & 0x01010101u) | (t1 & 0x04040404u) |
-			                    ((t2 << 2) & 0x10101010u) | ((t3 << 4) & 0x40404040u);
-			const uint32_t F = transpose2x4x4(Im);
+			const uint32_t F = invalid_flags(t0, t1, t2, t3, b0, b1, b2, b3);
 			const int j0 = (int)((uint32_t)__builtin_ctz(F) >> 1);          // first invalid base
 			const int j1 = (int)((31u - (uint32_t)__builtin_clz(F)) >> 1);  // last invalid base
 			V &= ~((2u << (15 - j0)) - 1u);          // windows ending at j >= j0
@@ -785,10 +803,7 @@ __device__ __forceinline__ void packed_streams(const VcKernelArgs &A, int c, int
 	const uint32_t anyinv = ((t0 | t1 | t2 | t3) & 0x04040404u) | ((b0 | b1 | b2 | b3) & 0x08080808u);
 	if (__ballot(anyinv != 0u)) {
 		if (anyinv != 0u) {   // as in packed_chunk: U moves to the last invalid base
-			t0 |= dec_bit3(b0); t1 |= dec_bit3(b1); t2 |= dec_bit3(b2); t3 |= dec_bit3(b3);
-			const uint32_t Im = ((t0 >> 2) & 0x01010101u) | (t1 & 0x04040404u) |
-			                    ((t2 << 2) & 0x10101010u) | ((t3 << 4) & 0x40404040u);
-			const uint32_t F = transpose2x4x4(Im);
+			const uint32_t F = invalid_flags(t0, t1, t2, t3, b0, b1, b2, b3);
 			const int j1 = (int)((31u - (uint32_t)__builtin_clz(F)) >> 1);
 			const int u1 = 16 - j1 - K;
 			U = U < u1 ? U : u1;
@@ -1196,10 +1211,7 @@ __device__ __forceinline__ uint32_t pack_fb(const Dir &D, uint32_t t0, uint32_t 
 __device__ __forceinline__ uint32_t invalid_bits_fb(const Dir &D, uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3,
                                                     uint32_t q0, uint32_t q1, uint32_t q2, uint32_t q3)
 {
-	t0 |= dec_bit3(q0); t1 |= dec_bit3(q1); t2 |= dec_bit3(q2); t3 |= dec_bit3(q3);
-	const uint32_t Im = ((t0 >> 2) & 0x01010101u) | (t1 & 0x04040404u) |
-	                    ((t2 << 2) & 0x10101010u) | ((t3 << 4) & 0x40404040u);
-	const uint32_t F = transpose2x4x4(Im);     // quad-order byte p at bit 2p
+	const uint32_t F = invalid_flags(t0, t1, t2, t3, q0, q1, q2, q3);   // quad-order byte p at bit 2p
 	// backwards: quad order -> read order (rotate by one dword), then reverse
 	return D.bwd ? pairrev(__builtin_amdgcn_alignbit(F, F, 8u)) : F;
 }
