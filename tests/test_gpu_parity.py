@@ -599,3 +599,13 @@ def test_reference_main_bound_to_libvafc(name, manifest, synth_dir, tmp_path):
         assert hashlib.md5(data).hexdigest() == entry["vaf_md5"]
         for key in ("bases", "seqs", "kmers"):
             assert stats.get(key) == entry["stats"].get(key), key
+
+
+def test_build_id_of_the_loaded_library(torch_dev):
+    """On the GPU box: the libvafc.so this process has loaded (the one every GPU
+    test here runs) carries the hash of this tree's sources, and so does every
+    CLI the tests run (tests/conftest.py refuses the session otherwise)."""
+    import vafc
+    want = vafc.tree_build_id()
+    assert vafc.lib().vc_build_id().decode() == want
+    vafc.check_build()
