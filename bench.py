@@ -499,11 +499,15 @@ def main():
         kmap.bind_outputs(par_counts.data_ptr(), par_tally.data_ptr())
         kmap.set_timing(False)
         kmap.count_device(p_seq.data_ptr(), n * L, p_offs.data_ptr(), p_lens.data_ptr(), n, stream)
+        torch.cuda.synchronize()
+        par_local = par_counts.cpu().numpy().view(np.uint32).copy()
         if world > 1:
             dist.all_reduce(par_counts)
             dist.all_reduce(par_tally)
         torch.cuda.synchronize()
         par = par_counts.cpu().numpy().view(np.uint32).copy()
+        log("rank %d: parity sample counted: local sum %d, after the all-reduce %d" % (
+            rank, int(par_local.astype(np.uint64).sum()), int(par.astype(np.uint64).sum())))
         kmap.bind_outputs(0, 0)
     if rank == 0 and not args.no_parity and n > 0:
         kind = "reference" if os.path.exists(REF_CLI) else "port"
@@ -548,8 +552,14 @@ def main():
                 db.write_vaf(par, gpu_vaf)
                 parity = md5(gpu_vaf) == md5(ref_vaf)
             else:            # N ranks counted the sample: N x the reference's counts
-                want = (vaf_counts(ref_vaf).astype(np.uint64) * world) & 0xFFFFFFFF
+                ref = vaf_counts(ref_vaf).astype(np.uint64)
+                want = (ref * world) & 0xFFFFFFFF
                 parity = bool(np.array_equal(par.astype(np.uint64), want))
+                log("parity sample: reference sum %d, x%d = %d; all-reduced sum %d; local rank-0 rows equal to "
+                    "the reference: %s; rows differing after the reduce: %d" % (
+                        int(ref.sum()), world, int(want.sum()), int(par.astype(np.uint64).sum()),
+                        bool(np.array_equal(par_local.astype(np.uint64), ref)),
+                        int((par.astype(np.uint64) != want).sum())))
         except Exception as e:  # the baseline must never hide the measured line
             log("cpu baseline failed: %r" % (e,))
     if rank == 0 and not args.no_e2e and args.config == "c2":
