@@ -366,6 +366,12 @@ def main():
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # Every torch op and every vafc launch of this process on one real stream:
+    # torch's default stream has the handle 0, which vc_count_device reads as
+    # "the counter's own stream" (non-blocking, no order with torch's work), so
+    # a zero-fill or a read generation on the default stream would race with
+    # the counting kernel.
+    torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if world > 1:
         backend = os.environ.get("VAFC_DIST_BACKEND", "nccl")
         if backend == "nccl":

@@ -10,7 +10,9 @@
 
 #include "vafc_common.h"
 
-#define VC_BLOCK 1024        // threads per block: 16 waves, one block per CU
+#ifndef VC_BLOCK
+#define VC_BLOCK 1024        // threads per block: 16 waves, one block per CU (-DVC_BLOCK=768 etc.: A/B)
+#endif
 #define VC_KV_FLANK 128      // kernel variant: flank-bitmap prefilter (vc_flank_*, k >= VC_FLANK_MIN_K)
 #define VC_QCAP 240          // per-wave LDS queue entries (u64): 16 waves x 1920 B + 128 KiB filter fit in 160 KiB
 
