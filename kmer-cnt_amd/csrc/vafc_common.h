@@ -116,6 +116,23 @@ VC_HD uint32_t vc_l2f_mask(uint32_t h2)
 	return (1u << (h2 & 31u)) | (1u << ((h2 >> 5) & 31u)) | (1u << ((h2 >> 10) & 31u));
 }
 
+/* Large panels (a second-level filter in use) and k >= 21: a larger LDS
+ * Bloom filter, VC_BIG_FILTER_WORDS 32-bit words (144 KiB: the queues shrink
+ * to VC_BIG_QCAP entries per wave to make room), not a power of two.  Word
+ * from the low 32 bits of the 40-bit product of the two strands' low 20 bits
+ * (the last ten bases of the window and of its reverse complement: for
+ * k >= 21 they exclude the centre base, so a SNP's ref and alt k-mers share
+ * the word) scaled to the word count by a multiply-high; the same two bits as
+ * the 32-bit-word filter.  On the 200k-SNP C5 panel the false-positive rate
+ * drops from 11.4 % (128 KiB) to 9.3 % (tools/c5_filter_fp.py). */
+#define VC_BIG_FILTER_WORDS 36860u
+#define VC_BIG_QCAP 128u
+VC_HD uint32_t vc_big_word(uint32_t flo, uint32_t rlo, uint32_t nwords)
+{
+	const uint32_t p = (flo & 0xFFFFFu) * (rlo & 0xFFFFFu);
+	return (uint32_t)(((uint64_t)p * nwords) >> 32);
+}
+
 /* Device key table slot: 16 bytes, one load per probe step. */
 typedef struct {
 	uint64_t key;

@@ -251,6 +251,9 @@ struct vc_ctx {
 	uint32_t l2bits = 0;
 	uint32_t fsh = 0;
 	uint32_t flank = 0;                    // the filter is the flank bitmap (vafc_common.h)
+	uint32_t big = 0;                      // the filter is the large-panel Bloom filter (vc_big_word)
+	uint32_t fwords = 0;                   // LDS filter words
+	uint32_t qcap = VC_QCAP;               // LDS queue entries per wave
 	uint32_t *d_counts = nullptr;          // active outputs (own or bound)
 	unsigned long long *d_tally = nullptr;
 	uint32_t *own_counts = nullptr;
@@ -374,6 +377,21 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	{
 		const char *fe = getenv("VAFC_FILTER");
 		const bool force_bloom = fe && !strcmp(fe, "bloom"), force_flank = fe && !strcmp(fe, "flank");
+		// large panels, k >= 21: the 144 KiB Bloom filter (vafc_common.h
+		// vc_big_word; the queues shrink to VC_BIG_QCAP); VAFC_FILTER=bloom128
+		// keeps the 128 KiB power-of-two filter (A/B and tests)
+		const bool force_b128 = fe && !strcmp(fe, "bloom128");
+		if (k >= VC_FLANK_MIN_K && l2bits && !force_b128) {
+			std::vector<uint32_t> fbig(VC_BIG_FILTER_WORDS, 0);
+			for (const vc_slot_t &e : tab)
+				if (e.key != VC_EMPTY_KEY) {
+					const uint32_t flo = (uint32_t)e.key, rlo = (uint32_t)vc_revcomp(e.key, k);
+					fbig[vc_big_word(flo, rlo, VC_BIG_FILTER_WORDS)] |= vc_filter_mask(flo, rlo);
+				}
+			fw.swap(fbig);
+			c->big = 1;
+			c->qcap = VC_BIG_QCAP;
+		}
 		if (k >= VC_FLANK_MIN_K && !l2bits && !force_bloom) {
 			std::vector<uint32_t> fb((size_t)1 << VC_FLANK_WBITS, 0);
 			for (const vc_slot_t &e : tab)
@@ -394,6 +412,7 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 	c->n_keys = inserted;
 	c->tbits = tbits;
 	c->wbits = wbits;
+	c->fwords = (uint32_t)fw.size();
 	c->l2bits = l2bits;
 	c->fsh = fsh;
 	c->ablate = getenv("VAFC_ABLATE") ? atoi(getenv("VAFC_ABLATE")) : 0;
@@ -579,6 +598,9 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 	A.wbits = c->wbits;
 	A.fsh = c->fsh;
 	A.flank = c->flank;
+	A.big = c->big;
+	A.fwords = c->fwords;
+	A.qcap = c->qcap;
 	A.l2f = c->d_l2f;
 	A.l2bits = c->l2bits;
 	A.ablate = c->ablate;
@@ -810,7 +832,7 @@ extern "C" int vc_table_info(const vc_ctx *c, uint64_t *n_keys, uint64_t *slots,
 	if (!c) return VC_EINVAL;
 	if (n_keys) *n_keys = c->n_keys;
 	if (slots) *slots = (uint64_t)1 << c->tbits;
-	if (filter_bytes) *filter_bytes = (uint64_t)4 << c->wbits;
+	if (filter_bytes) *filter_bytes = (uint64_t)4 * c->fwords;
 	return VC_OK;
 }
 

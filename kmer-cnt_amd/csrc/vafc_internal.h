@@ -14,6 +14,7 @@
 #define VC_BLOCK 1024        // threads per block: 16 waves, one block per CU (-DVC_BLOCK=768 etc.: A/B)
 #endif
 #define VC_KV_FLANK 128      // kernel variant: flank-bitmap prefilter (vc_flank_*, k >= VC_FLANK_MIN_K)
+#define VC_KV_BIG 512        // kernel variant: large-panel Bloom filter (vc_big_word, k >= VC_FLANK_MIN_K)
 #define VC_QCAP 240          // per-wave LDS queue entries (u64): 16 waves x 1920 B + 128 KiB filter fit in 160 KiB
 
 struct VcKernelArgs {
@@ -29,6 +30,9 @@ struct VcKernelArgs {
 	uint32_t wbits;
 	uint32_t fsh;                // filter word shift (vc_filter_shift)
 	uint32_t flank;              // 1: the filter is the flank bitmap (vc_flank_*), not the Bloom filter
+	uint32_t big;                // 1: the large-panel Bloom filter (vc_big_word, fwords words)
+	uint32_t fwords;             // LDS filter words (2^wbits, or VC_BIG_FILTER_WORDS)
+	uint32_t qcap;               // LDS queue entries per wave (VC_QCAP, or VC_BIG_QCAP)
 	const uint32_t *l2f;         // second-level filter (vc_l2f_*), NULL = off
 	uint32_t l2bits;
 	int ablate;                  // ablation builds only (VAFC_ABLATE), 0 otherwise
@@ -45,10 +49,10 @@ struct VcKernelArgs {
 };
 
 // LDS: prefilter words + 4 zero words (16-byte aligned), then the per-wave queues.
-__host__ __device__ static inline uint32_t vc_filter_lds_words(uint32_t wbits) { return (1u << wbits) + 4u; }
-static inline size_t vc_lds_bytes(uint32_t wbits)
+__host__ __device__ static inline uint32_t vc_filter_lds_words(uint32_t fwords) { return fwords + 4u; }
+static inline size_t vc_lds_bytes(uint32_t fwords, uint32_t qcap)
 {
-	return (size_t)4 * vc_filter_lds_words(wbits) + (size_t)(VC_BLOCK / 64) * VC_QCAP * 8;
+	return (size_t)4 * vc_filter_lds_words(fwords) + (size_t)(VC_BLOCK / 64) * qcap * 8;
 }
 
 #ifdef __cplusplus

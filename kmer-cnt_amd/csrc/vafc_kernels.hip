@@ -147,7 +147,11 @@ extern "C" hipError_t vc_launch_count(const VcKernelArgs *A, int grid, int grid_
 
 extern "C" hipError_t vc_kernel_setup(void)
 {
-	const int lds = (int)vc_lds_bytes(VC_MAX_FILTER_WBITS);
+	// the largest dynamic LDS any launch asks for: the 128 KiB filter with full
+	// queues, or the large-panel filter with short ones (exactly 160 KiB)
+	const size_t l128 = vc_lds_bytes(1u << VC_MAX_FILTER_WBITS, VC_QCAP);
+	const size_t lbig = vc_lds_bytes(VC_BIG_FILTER_WORDS, VC_BIG_QCAP);
+	const int lds = (int)(l128 > lbig ? l128 : lbig);
 	hipError_t e = setup_k<0>(lds);
 #define VC_K_SET(k) if (e == hipSuccess) e = vc_setup_k##k(lds);
 	VC_K_LIST(VC_K_SET)

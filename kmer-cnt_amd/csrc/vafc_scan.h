@@ -197,7 +197,7 @@ __device__ __forceinline__ void probe_and_count(const VcKernelArgs &A, uint64_t 
 }
 
 struct WaveQueue {
-	uint64_t *q;     // LDS, VC_QCAP entries
+	uint64_t *q;     // LDS, A.qcap entries
 	uint32_t n;      // wave-uniform fill
 };
 
@@ -297,7 +297,7 @@ __device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q
 	                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
 	if (hit) Q.q[Q.n + pre] = key;
 	Q.n = __builtin_amdgcn_readfirstlane(Q.n + (uint32_t)__popcll(bal));
-	if (Q.n > VC_QCAP - WAVE) {
+	if (Q.n > A.qcap - WAVE) {        // A.qcap >= 2 WAVE
 		drain_range(A, Q.q, Q.n - WAVE, Q.n, lane);
 		Q.n -= WAVE;
 		// leave nothing in flight on this (rare) path, so that the compiler
@@ -386,7 +386,7 @@ __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t 
                                           WaveQueue &Q, uint32_t &tl, int lane)
 {
 	const uint32_t fsh = A.fsh;
-	const uint32_t zero_word = 1u << A.wbits;   // an all-zero LDS word past the filter
+	const uint32_t zero_word = A.fwords;        // an all-zero LDS word past the filter
 	// the read's tail chunk decodes with seq_nt4_table (vaf-counter.c:261-291);
 	// in seq_nt4 mode (snp-pattern-gen) every chunk does: tail_c = -1 and the
 	// test (c | -1) == -1 always holds (the OR is scalar in the reads kernel)
@@ -636,6 +636,81 @@ __device__ __forceinline__ uint32_t flank_bits(uint32_t fbase, uint32_t Bm1, uin
 	return R0 | R1;
 }
 
+// Large-panel Bloom filter (VC_KV_BIG, vc_big_word): per window the strands'
+// low 20 bits, each ONE v_bfe_u32 of a register that holds the whole field --
+// the forward stream's 10-mer ending at base j (Bc, or one of two registers
+// over (B[c-1]:B[c]) starting at bases -9 and -7), and the complement
+// stream's ten bases from the window's first (C[c-2], C[c-1], C[c], or up to
+// two more registers placed by BigPlan) -- then the 40-bit product's low word,
+// a multiply-high by the word count and the same two-bit test as the
+// 32-bit-word filter.  9 VALU per window plus about 4 per chunk, as for the
+// power-of-two filter (2 v_alignbit, multiply, shift, and-or).
+template <int K> struct BigPlan {
+	int co[16];      // start (chunk-relative base) of the C-stream register for window j
+	constexpr BigPlan() : co{}
+	{
+		bool cov[16] = {};
+		const int free_o[3] = {0, -16, -32};
+		for (int j = 0; j < 16; ++j) {
+			const int q0 = j - K + 1;
+			for (int f = 0; f < 3; ++f)
+				if (!cov[j] && free_o[f] <= q0 && q0 <= free_o[f] + 6) {
+					co[j] = free_o[f];
+					cov[j] = true;
+				}
+		}
+		for (int j = 0; j < 16; ++j)
+			if (!cov[j]) {
+				const int o = j - K + 1;
+				for (int jj = j; jj < 16; ++jj)
+					if (!cov[jj] && jj - K + 1 <= o + 6) {
+						co[jj] = o;
+						cov[jj] = true;
+					}
+			}
+	}
+};
+
+// The C-stream register (base p of chunks c-2, c-1, c at bit 2(p + 32) of
+// Cc:Cm1:Cm2) that starts at base o, o in [-32, 0] (a constant after unrolling).
+__device__ __forceinline__ uint32_t c_reg(int o, uint32_t Cm2, uint32_t Cm1, uint32_t Cc)
+{
+	if (o == -32) return Cm2;
+	if (o == -16) return Cm1;
+	if (o == 0) return Cc;
+	if (o < -16) return __builtin_amdgcn_alignbit(Cm1, Cm2, (uint32_t)(2 * (o + 32)));
+	return __builtin_amdgcn_alignbit(Cc, Cm1, (uint32_t)(2 * (o + 16)));
+}
+
+template <int K, int J0, int J1, int ABL>
+__device__ __forceinline__ uint32_t bloom_bits_big(const VcKernelArgs &A, uint32_t fbase, uint32_t Bm1, uint32_t Bc,
+                                                  uint32_t Cm2, uint32_t Cm1, uint32_t Cc)
+{
+	constexpr BigPlan<K> plan{};
+	const uint32_t nw4 = A.fwords << 2;
+	const uint32_t B9 = __builtin_amdgcn_alignbit(Bm1, Bc, 18u);    // bases -9 .. 6
+	const uint32_t B7 = __builtin_amdgcn_alignbit(Bm1, Bc, 14u);    // bases -7 .. 8
+	uint32_t fw[16], fl[16], rl[16];
+#pragma unroll
+	for (int j = J0; j < J1; ++j) {
+		const int bo = j >= 9 ? 0 : (j <= 6 ? -9 : -7);             // B register holding the 10-mer ending at j
+		const uint32_t bsrc = bo == 0 ? Bc : (bo == -9 ? B9 : B7);
+		const uint32_t f20 = __builtin_amdgcn_ubfe(bsrc, (uint32_t)(2 * (bo + 15 - j)), 20u);
+		const int co = plan.co[j];
+		const uint32_t r20 = __builtin_amdgcn_ubfe(c_reg(co, Cm2, Cm1, Cc), (uint32_t)(2 * (j - K + 1 - co)), 20u);
+		const uint32_t a = __umulhi(f20 * r20, nw4) & ~3u;
+		if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(a)); fw[j] = a; }
+		else fw[j] = *(lds_u32_t *)(uintptr_t)(a | fbase);
+		fl[j] = f20;
+		rl[j] = r20;
+	}
+	uint32_t hm = 0;
+#pragma unroll
+	for (int j = J0; j < J1; ++j) hm = (hm << 1) | ((fw[j] >> (fl[j] & 31u)) & (fw[j] >> (rl[j] & 31u)) & 1u);
+	if constexpr (J1 < 16) hm <<= 16 - J1;
+	return hm;
+}
+
 // One 16-base chunk c of the packed scan from its five dwords (w0: the dword
 // holding the chunk's first byte, realigned by sh); (B1, C1) / (B2, C2) are
 // the streams of chunks c-1 / c-2 and move on to c / c-1.
@@ -677,6 +752,9 @@ __device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, i
 		const uint32_t P = (H << 16) | hm;           // R of chunks c-1 | c, c-2 in H >> 16
 		hm &= __builtin_amdgcn_alignbit(H >> 16, P, (uint32_t)(K - VC_FLANK_BASES));
 		H = P;
+	} else if constexpr ((ABL & VC_KV_BIG) != 0) {
+		(void)fsh; (void)wmask4;
+		hm = bloom_bits_big<K, J0, J1, ABL>(A, fbase, Bm1, Bc, Cm2, Cm1, Cc);
 	} else {
 	// pass <=> bits (flo & 31) and (rlo & 31) of the filter word are set:
 	// hm = (hm << 1) | ((w >> flo) & (w >> rlo) & 1), 4 VALU per window
@@ -1496,7 +1574,7 @@ __device__ __forceinline__ void scan_any(const VcKernelArgs &A, const uint32_t *
 
 __device__ __forceinline__ void load_filter(const VcKernelArgs &A, uint32_t *filt)
 {
-	const uint32_t nw = 1u << A.wbits;
+	const uint32_t nw = A.fwords;        // a multiple of 4
 	const uint4 *src = reinterpret_cast<const uint4 *>(A.filter);
 	uint4 *dst = reinterpret_cast<uint4 *>(filt);
 	for (uint32_t i = threadIdx.x; i < nw / 4u; i += blockDim.x) dst[i] = src[i];
@@ -1520,7 +1598,7 @@ vc_count_reads_kernel(VcKernelArgs A)
 	const int lane = threadIdx.x & (WAVE - 1);
 	const int wave = threadIdx.x / WAVE;
 	WaveQueue Q;
-	Q.q = reinterpret_cast<uint64_t *>(smem + vc_filter_lds_words(A.wbits)) + wave * VC_QCAP;
+	Q.q = reinterpret_cast<uint64_t *>(smem + vc_filter_lds_words(A.fwords)) + wave * A.qcap;
 	Q.n = 0;
 	load_filter(A, filt);
 
@@ -1570,7 +1648,7 @@ vc_count_reads_kernel(VcKernelArgs A)
 		// (two per lane): each drain exposes one probe latency, so fewer, fuller
 		// drains cost less (C2: -1.6 %, C5: +-0; ABL 64 = a drain per group)
 		if constexpr ((ABL & 64) != 0) queue_flush(A, Q, lane);
-		else if (Q.n > VC_QCAP - 2 * WAVE) queue_flush(A, Q, lane);
+		else if ((int)Q.n > (int)A.qcap - 2 * WAVE) queue_flush(A, Q, lane);
 		g = gn;
 		r = rn;
 	}
@@ -1596,7 +1674,7 @@ vc_count_long_kernel(VcKernelArgs A)
 	const int lane = threadIdx.x & (WAVE - 1);
 	const int wave = threadIdx.x / WAVE;
 	WaveQueue Q;
-	Q.q = reinterpret_cast<uint64_t *>(smem + vc_filter_lds_words(A.wbits)) + wave * VC_QCAP;
+	Q.q = reinterpret_cast<uint64_t *>(smem + vc_filter_lds_words(A.fwords)) + wave * A.qcap;
 	Q.n = 0;
 	load_filter(A, filt);
 
@@ -1640,11 +1718,12 @@ vc_count_long_kernel(VcKernelArgs A)
 template <int K, int ABL = 0>
 static hipError_t launch_kw(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
 {
-	const size_t lds = vc_lds_bytes(A->wbits);
+	const size_t lds = vc_lds_bytes(A->fwords, A->qcap);
 	hipLaunchKernelGGL((vc_count_reads_kernel<K, ABL>), dim3(grid), dim3(VC_BLOCK), lds, st, *A);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return e;
-	hipLaunchKernelGGL((vc_count_long_kernel<K, ABL & VC_KV_FLANK>), dim3(grid_long), dim3(VC_BLOCK), lds, st, *A);
+	hipLaunchKernelGGL((vc_count_long_kernel<K, ABL & (VC_KV_FLANK | VC_KV_BIG)>), dim3(grid_long), dim3(VC_BLOCK),
+	                   lds, st, *A);
 	return hipGetLastError();
 }
 
@@ -1668,8 +1747,10 @@ static hipError_t launch_k(const VcKernelArgs *A, int grid, int grid_long, hipSt
 		}
 	}
 #endif
-	if constexpr (K >= VC_FLANK_MIN_K)
+	if constexpr (K >= VC_FLANK_MIN_K) {
 		if (A->flank) return launch_kw<K, VC_KV_FLANK>(A, grid, grid_long, st);
+		if (A->big) return launch_kw<K, VC_KV_BIG>(A, grid, grid_long, st);
+	}
 	return launch_kw<K>(A, grid, grid_long, st);
 }
 
@@ -1687,6 +1768,12 @@ static hipError_t setup_k(int lds)
 			                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 		if (e == hipSuccess)
 			e = hipFuncSetAttribute((const void *)vc_count_long_kernel<K, VC_KV_FLANK>,
+			                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+		if (e == hipSuccess)
+			e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<K, VC_KV_BIG>,
+			                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+		if (e == hipSuccess)
+			e = hipFuncSetAttribute((const void *)vc_count_long_kernel<K, VC_KV_BIG>,
 			                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 	}
 #ifdef VC_ABLATION
