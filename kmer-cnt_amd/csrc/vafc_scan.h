@@ -46,6 +46,11 @@
 #else
 #define VC_FLANK_U8 1          // flank lookups: bytes, two v_bfe_u32 of one register
 #endif
+#ifdef VC_DEFER_BIG
+#define VC_KV_BIG_DEFER VC_KV_BIG   // large-panel kernels: one hit loop per chunk pair
+#else
+#define VC_KV_BIG_DEFER 0
+#endif
 #ifdef VC_SCAN_BWD
 #define VC_SCAN_FB 1           // odd lanes scan backwards (scan_span_quad_fb; measured slower)
 #else
@@ -1147,11 +1152,12 @@ __device__ __forceinline__ void scan_span_quad(const VcKernelArgs &A, const uint
 		// flank mode: one hit loop per chunk pair (the Bloom-filter kernels are
 		// at the 128-VGPR limit and would spill; ablation builds: A.variant
 		// bit 6 = per chunk)
-		bool defer = (ABL & VC_KV_FLANK) != 0;
+		// (the large-panel Bloom kernels too: VC_DEFER_BIG, A/B)
+		bool defer = (ABL & (VC_KV_FLANK | VC_KV_BIG_DEFER)) != 0;
 #ifdef VC_ABLATION
 		defer = defer && (A.variant & 64u) == 0;
 #endif
-		if constexpr ((ABL & VC_KV_FLANK) == 0) defer = false;
+		if constexpr ((ABL & (VC_KV_FLANK | VC_KV_BIG_DEFER)) == 0) defer = false;
 		if (defer) {
 #pragma unroll
 			for (int p = 0; p < 2; ++p) {
