@@ -586,22 +586,21 @@ __device__ __forceinline__ int clamp16(int v) { return v < 0 ? 0 : (v > 16 ? 16 
 // is the same bytes read one byte at a time, byte v >> 3, bit v & 7.  The
 // byte address (bits 3..19 of the 10-mer) and the bit index (bits 0..2) are
 // two v_bfe_u32 of ONE register that holds the whole 10-mer: Bc for bases
-// 9..15, M7 = bases -8..7 for bases 1..7, M8 = bases -7..8 for base 8 and
-// M0 = bases -15..0 for base 0 (three v_alignbit per chunk).  4 VALU per base
-// plus 3 per chunk, against 5 per base: no per-base extraction, and no mask
-// (the byte address needs none; the 32-bit word address needed shift + mask).
+// 9..15, B7 = bases -7..8 for bases 7 and 8, B9 = bases -9..6 for bases 0..6
+// (two v_alignbit per chunk).  4 VALU per base plus 2 per chunk, against 5
+// per base: no per-base extraction, and no mask (the byte address needs none;
+// the 32-bit word address needed shift + mask).
 template <int J0, int J1, int ABL = 0>
 __device__ __forceinline__ uint32_t flank_bits_u8(uint32_t Bm1, uint32_t Bc)
 {
 	typedef const uint8_t __attribute__((address_space(3))) lds_u8_t;
-	const uint32_t M7 = J0 <= 7 && J1 > 1 ? __builtin_amdgcn_alignbit(Bm1, Bc, 16u) : 0u;
-	const uint32_t M8 = J0 <= 8 && J1 > 8 ? __builtin_amdgcn_alignbit(Bm1, Bc, 14u) : 0u;
-	const uint32_t M0 = J0 == 0 ? __builtin_amdgcn_alignbit(Bm1, Bc, 30u) : 0u;
+	const uint32_t B9 = J0 <= 6 ? __builtin_amdgcn_alignbit(Bm1, Bc, 18u) : 0u;              // bases -9 .. 6
+	const uint32_t B7 = J0 <= 8 && J1 > 7 ? __builtin_amdgcn_alignbit(Bm1, Bc, 14u) : 0u;   // bases -7 .. 8
 	uint32_t fb[16], fi[16];
 #pragma unroll
 	for (int j = J0; j < J1; ++j) {
-		const uint32_t src = j >= 9 ? Bc : (j == 8 ? M8 : (j >= 1 ? M7 : M0));
-		const uint32_t s = j >= 9 ? 2u * (15 - j) : (j == 8 || j == 0 ? 0u : 2u * (7 - j));
+		const uint32_t src = j >= 9 ? Bc : (j >= 7 ? B7 : B9);
+		const uint32_t s = j >= 9 ? 2u * (15 - j) : (j >= 7 ? 2u * (8 - j) : 2u * (6 - j));
 		const uint32_t a = __builtin_amdgcn_ubfe(src, s + 3u, 2 * VC_FLANK_BASES - 3);
 		fi[j] = __builtin_amdgcn_ubfe(src, s, 3u);
 		if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(a)); fb[j] = a; }
