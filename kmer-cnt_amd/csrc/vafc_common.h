@@ -77,26 +77,35 @@ VC_HD uint32_t vc_filter_word(uint32_t flo, uint32_t rlo, uint32_t fsh, uint32_t
 VC_HD uint32_t vc_filter_mask(uint32_t flo, uint32_t rlo) { return (1u << (flo & 31u)) | (1u << (rlo & 31u)); }
 
 /* Flank bitmap (k >= 21, small panels): an exact 2^20-bit set S of 10-mers,
- * 128 KiB of LDS, holding the first and the last ten bases of every key and
- * of its reverse complement.  S is closed under reverse complement, so a
- * window that is a key in either orientation has its forward first and last
- * 10-mers in S: the kernel looks up the forward 10-mer ending at every base
- * once and ANDs the bits of each window's two ends -- a necessary condition,
- * 5 VALU per base instead of ~9.5 per window for the Bloom filter.  For
- * k >= 21 the two 10-mers exclude the centre base, so a SNP's ref and alt
- * k-mers share all four entries.  A random window passes with about the
- * square of S's density (the GRCh38 panel: 7.7 %, 0.59 %).
- * 10-mer v (20 bits, first base high, the k-mer encoding): word v >> 5, bit
- * v & 31. */
+ * 128 KiB of LDS, holding four 10-mers of every key and of its reverse
+ * complement: the ones ending at distances VC_FLANK_DIST(k, t), t = 0..3,
+ * before the key's last base (t = 0: its last ten bases, t = 3: its first
+ * ten, t = 1, 2: evenly between).  S is closed under reverse complement
+ * (the distances are symmetric: d(t) + d(3 - t) = k - 10), so a window that
+ * is a key in either orientation has all four of its forward 10-mers in S.
+ * The kernel looks up the forward 10-mer ending at every base once and ANDs
+ * the four bits of each window -- a necessary condition, 4 VALU per base
+ * plus about 4 per 16 windows.  For k >= 21 the first and last 10-mers
+ * exclude the centre base (the middle two do not; a SNP's ref and alt
+ * k-mers then add separate middle entries).  A random window passes with
+ * about the fourth power of S's density: on the GRCh38 panel (k = 21) 21 %
+ * of S is set and 0.22 % of the benchmark's windows pass (1.6 % of which
+ * are true hits), against 7.7 % and 0.59 % with the first and last 10-mers
+ * alone (tools/flank_fp.py).
+ * 10-mer v (20 bits, first base high, the k-mer encoding): byte v >> 3,
+ * bit v & 7 (= word v >> 5, bit v & 31 on a little-endian word array). */
 #define VC_FLANK_BASES 10
 #define VC_FLANK_MIN_K 21
 #define VC_FLANK_WBITS (2 * VC_FLANK_BASES - 5)  /* 2^15 words */
+#define VC_FLANK_TESTS 4
+#define VC_FLANK_DIST(k, t) (((t) * ((k) - VC_FLANK_BASES) + 1) / 3)
 VC_HD void vc_flank_mark(uint32_t *bm, uint64_t kmer, int k)
 {
 	const uint32_t m = (1u << (2 * VC_FLANK_BASES)) - 1u;
-	const uint32_t last = (uint32_t)kmer & m, first = (uint32_t)(kmer >> (2 * k - 2 * VC_FLANK_BASES)) & m;
-	bm[last >> 5] |= 1u << (last & 31u);
-	bm[first >> 5] |= 1u << (first & 31u);
+	for (int t = 0; t < VC_FLANK_TESTS; ++t) {
+		const uint32_t v = (uint32_t)(kmer >> (2 * VC_FLANK_DIST(k, t))) & m;
+		bm[v >> 5] |= 1u << (v & 31u);
+	}
 }
 
 /* Second-level filter for large key sets (> 2^16 keys, where the LDS

@@ -371,8 +371,8 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 		++inserted;
 	}
 	// flank bitmap instead of the Bloom filter (vafc_common.h) for k >= 21 and
-	// no second level, when a random window's pass rate (about the square of
-	// the bitmap's density) stays under 1 %; VAFC_FILTER=bloom|flank forces
+	// no second level, when a random window's pass rate (about the fourth
+	// power of the bitmap's density) stays under 1 %; VAFC_FILTER=bloom|flank forces
 	// one (A/B and tests; flank only where k allows it)
 	{
 		const char *fe = getenv("VAFC_FILTER");
@@ -402,7 +402,7 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 			uint64_t set = 0;
 			for (uint32_t w : fb) set += (uint64_t)__builtin_popcount(w);
 			const double dens = (double)set / (double)((uint64_t)1 << (2 * VC_FLANK_BASES));
-			if (force_flank || dens <= 0.10) {
+			if (force_flank || dens * dens * dens * dens <= 0.01) {
 				fw.swap(fb);
 				wbits = VC_FLANK_WBITS;
 				c->flank = 1;

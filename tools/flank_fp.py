@@ -1,29 +1,93 @@
 #!/usr/bin/env python3
-"""Pass rate of the flank-bitmap prefilter (vafc_common.h vc_flank_mark) on the
-benchmark panel, CPU only: the exact 2^20-bit set of every key's first and
-last ten bases (both strands), queried with 4M uniform random k-mers.
+"""Pass rate of the flank-bitmap prefilter (vafc_common.h vc_flank_mark,
+VC_FLANK_DIST) on the benchmark panel, CPU only (tools, not tests).
+
+The bitmap is the exact 2^20-bit set of the 10-mers of every key and of its
+reverse complement that end at the test distances before the key's last base;
+a window passes iff its own 10-mers at those distances are all set.  Two
+forms: the round-2 one (first and last ten bases, distances 0 and k - 10) and
+the four-test one of the kernels (distances VC_FLANK_DIST(k, 0..3)).  Each is
+queried with 4M uniform random k-mers and with the valid windows of 200k
+benchmark reads (C2's generator: 1 % of reads drawn over a SNP, so some
+passes are true hits; "true" = windows that are keys).
     python tools/flank_fp.py
 """
-import os, sys, tempfile
+import os
+import sys
+import tempfile
+
 import numpy as np
-ROOT=os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, os.path.join(ROOT,"kmer-cnt_amd")); sys.path.insert(0, os.path.join(ROOT,"tools"))
-import vafc, vafc_synth as S
-def revcomp(x,K):
-    r=np.zeros_like(x)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kmer-cnt_amd"))
+import vafc  # noqa: E402
+import vafc_synth as S  # noqa: E402
+
+M = np.uint64((1 << 20) - 1)
+
+
+def revcomp(x, K):
+    r = np.zeros_like(x)
     for _ in range(K):
-        r=(r<<np.uint64(2))|(np.uint64(3)-(x&np.uint64(3))); x=x>>np.uint64(2)
+        r = (r << np.uint64(2)) | (np.uint64(3) - (x & np.uint64(3)))
+        x = x >> np.uint64(2)
     return r
-panel=S.make_panel(S.read_bed(S.default_bed_path()))
-for K in (21,31,25,17):
-    d=tempfile.mkdtemp(); pat=os.path.join(d,"p.txt"); panel.write_patterns(pat,K)
-    keys,_,_=vafc.load_patterns(pat).keys(K)
-    keys=np.unique(np.asarray(keys,dtype=np.uint64))
-    allk=np.concatenate([keys,revcomp(keys,K)])
-    M=np.uint64((1<<20)-1)
-    last=allk&M; first=(allk>>np.uint64(2*K-20))&M
-    bm=np.zeros(1<<20,bool); bm[last]=True; bm[first]=True
-    dens=bm.mean()
-    q=np.random.default_rng(1).integers(0,1<<(2*K),size=4_000_000,dtype=np.uint64)
-    ql=q&M; qf=(q>>np.uint64(2*K-20))&M
-    fp=(bm[ql]&bm[qf]).mean()
-    print(K,"keys",len(keys),"distinct10",bm.sum(),"density %.4f"%dens,"FP %.4f%%"%(100*fp))
+
+
+def dists(K, tests):
+    if tests == 2:
+        return (0, K - 10)
+    return tuple((t * (K - 10) + 1) // 3 for t in range(4))   # VC_FLANK_DIST
+
+
+def read_windows(reads, K):
+    """Forward k-mers of the valid windows of reads (uint8 ASCII rows)."""
+    lut = np.full(256, 4, np.int64)
+    for c, v in zip(b"ACGT", range(4)):
+        lut[c] = v
+    codes = lut[reads]
+    bad = codes == 4
+    cz = np.where(bad, 0, codes).astype(np.uint64)
+    n, L = codes.shape
+    mk = np.uint64((1 << (2 * K)) - 1) if K < 32 else np.uint64(-1)
+    acc = np.zeros(n, np.uint64)
+    out = []
+    run = np.zeros(n, np.int64)
+    for p in range(L):
+        acc = ((acc << np.uint64(2)) | cz[:, p]) & mk
+        run = np.where(bad[:, p], 0, run + 1)
+        if p >= K - 1:
+            out.append(acc[run >= K])
+    return np.concatenate(out)
+
+
+def main():
+    panel = S.make_panel(S.read_bed(S.default_bed_path()))
+    reads = S.gen_reads(panel, 200_000)
+    for K in (21, 25, 31):
+        d = tempfile.mkdtemp()
+        pat = os.path.join(d, "p.txt")
+        panel.write_patterns(pat, K)
+        keys, _, _ = vafc.load_patterns(pat).keys(K)
+        keys = np.unique(np.asarray(keys, dtype=np.uint64))
+        allk = np.concatenate([keys, revcomp(keys, K)])
+        q = np.random.default_rng(1).integers(0, 1 << (2 * K), size=4_000_000, dtype=np.uint64)
+        win = read_windows(reads, K)
+        true = np.isin(win, allk).mean()
+        for tests in (2, 4):
+            ds = dists(K, tests)
+            bm = np.zeros(1 << 20, bool)
+            for dd in ds:
+                bm[(allk >> np.uint64(2 * dd)) & M] = True
+
+            def passes(x):
+                ok = np.ones(x.size, bool)
+                for dd in ds:
+                    ok &= bm[(x >> np.uint64(2 * dd)) & M]
+                return ok.mean()
+            print("k=%d tests=%d distances=%s keys %d density %.4f random %.4f%% reads %.4f%% (true hits %.4f%%)"
+                  % (K, tests, ds, len(keys), bm.mean(), 100 * passes(q), 100 * passes(win), 100 * true))
+
+
+if __name__ == "__main__":
+    main()
