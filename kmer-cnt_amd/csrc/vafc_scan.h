@@ -123,6 +123,53 @@ __device__ __forceinline__ uint32_t dec_tail(uint32_t b)
 	return (t & ~sel) | (b & sel);
 }
 
+// Tail decode of 4 bytes from their head codes t = dec_code(b): the same
+// result as dec_tail in 10 VALU instead of 17.  A byte is a valid letter iff
+// (b & 0xDF) equals the upper-case ACGTU letter expected for its low three
+// bits (EXP_*; 0xFF never matches, and a set bit 3 or bit 7 never matches);
+// its code is then the head code.  Bytes 0..3 map to themselves (a rare
+// branch).  tests/test_gpu_parity.py::test_tail_bytes_vs_oracle.
+#define EXP_LO 0x43FF41FFu   // low bits 0..3: -, 'A', -, 'C'
+#define EXP_HI 0x47FF5554u   // low bits 4..7: 'T', 'U', -, 'G'
+__device__ __forceinline__ uint32_t dec_tail_from(uint32_t b, uint32_t t)
+{
+	const uint32_t e = __builtin_amdgcn_perm(EXP_HI, EXP_LO, b & 0x07070707u);
+	const uint32_t d = (b & 0xDFDFDFDFu) ^ e;
+	const uint32_t bad = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;   // byte is no letter
+	t |= bad >> 5;
+	const uint32_t big = (((b & 0x7C7C7C7Cu) + 0x7F7F7F7Fu) | b) & 0x80808080u;   // byte >= 4
+	if (__ballot(big != 0x80808080u)) {
+		if (big != 0x80808080u) {
+			const uint32_t sel = ((~big & 0x80808080u) >> 7) * 0xFFu;
+			t = (t & ~sel) | (b & sel);
+		}
+	}
+	return t;
+}
+
+// The tail chunk of a read (cm == tail_c; tail_r = len & 15 bytes of it are
+// the read's): t_m = dec_code(b_m) on entry, tail semantics for the dwords
+// that hold tail bytes of some lane of the wave.  Dwords past every tail
+// lane's last byte keep their head codes: they decode bytes past the read's
+// end, whose windows are outside the read (masked by V) and whose invalid
+// flags only move U for chunks that do not exist.
+__device__ __forceinline__ void dec_tail_chunk(bool tl, int tail_r, uint32_t b0, uint32_t b1, uint32_t b2,
+                                               uint32_t b3, uint32_t &t0, uint32_t &t1, uint32_t &t2, uint32_t &t3)
+{
+	if (__ballot(tl)) {
+		if (tl) t0 = dec_tail_from(b0, t0);
+		if (__ballot(tl && tail_r > 4)) {
+			if (tl) t1 = dec_tail_from(b1, t1);
+			if (__ballot(tl && tail_r > 8)) {
+				if (tl) t2 = dec_tail_from(b2, t2);
+				if (__ballot(tl && tail_r > 12)) {
+					if (tl) t3 = dec_tail_from(b3, t3);
+				}
+			}
+		}
+	}
+}
+
 // Invalid-flag mask for the bytes of a word whose first position is P, given
 // the valid position range [lo, hi): bytes outside get bit 2 set.
 __device__ __forceinline__ uint32_t range_mask_hi(int rel_hi)
@@ -735,7 +782,7 @@ __device__ __forceinline__ uint32_t bloom_bits_big(const VcKernelArgs &A, uint32
 // holding the chunk's first byte, realigned by sh); (B1, C1) / (B2, C2) are
 // the streams of chunks c-1 / c-2 and move on to c / c-1.
 template <int K, int ABL, int J0 = 0, int J1 = 16, bool DEFER = false>
-__device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, int tail_c, int nt4m, uint32_t sh,
+__device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, int tail_c, int tail_r, int nt4m, uint32_t sh,
                                              uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
                                              uint32_t &Bm1, uint32_t &Bm2, uint32_t &Cm1, uint32_t &Cm2,
                                              int &U, int &Qe, uint32_t &H, const uint32_t *__restrict__ filt,
@@ -750,10 +797,7 @@ __device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, i
 	const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
 	const uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
 	uint32_t t0 = dec_code(b0), t1 = dec_code(b1), t2 = dec_code(b2), t3 = dec_code(b3);
-	const int cm = c | nt4m;
-	if (__ballot(cm == tail_c)) {
-		if (cm == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
-	}
+	dec_tail_chunk((c | nt4m) == tail_c, tail_r, b0, b1, b2, b3, t0, t1, t2, t3);
 	U += 16;
 	Qe += 16;
 	constexpr bool FL = (ABL & VC_KV_FLANK) != 0;
@@ -880,7 +924,7 @@ __device__ __forceinline__ void hit_loop2(const VcKernelArgs &A, WaveQueue &Q, u
 // the windows that span it) and the stream rotation of packed_chunk, without
 // its 16 filter lookups, validity mask, tally or hit loop.
 template <int K, int ABL>
-__device__ __forceinline__ void packed_streams(const VcKernelArgs &A, int c, int tail_c, int nt4m, uint32_t sh, uint32_t w0, uint32_t w1,
+__device__ __forceinline__ void packed_streams(const VcKernelArgs &A, int c, int tail_c, int tail_r, int nt4m, uint32_t sh, uint32_t w0, uint32_t w1,
                                                uint32_t w2, uint32_t w3, uint32_t w4, uint32_t &Bm1, uint32_t &Bm2,
                                                uint32_t &Cm1, uint32_t &Cm2, int &U, int &Qe, uint32_t &H,
                                                const uint32_t *__restrict__ filt)
@@ -890,10 +934,7 @@ __device__ __forceinline__ void packed_streams(const VcKernelArgs &A, int c, int
 	const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
 	const uint32_t b3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
 	uint32_t t0 = dec_code(b0), t1 = dec_code(b1), t2 = dec_code(b2), t3 = dec_code(b3);
-	const int cm = c | nt4m;
-	if (__ballot(cm == tail_c)) {
-		if (cm == tail_c) { t0 = dec_tail(b0); t1 = dec_tail(b1); t2 = dec_tail(b2); t3 = dec_tail(b3); }
-	}
+	dec_tail_chunk((c | nt4m) == tail_c, tail_r, b0, b1, b2, b3, t0, t1, t2, t3);
 	U += 16;
 	Qe += 16;
 	constexpr bool FL = (ABL & VC_KV_FLANK) != 0;
@@ -983,6 +1024,7 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	// in seq_nt4 mode (snp-pattern-gen) every chunk does: tail_c = -1 and the
 	// test (c | -1) == -1 always holds (the OR is scalar in the reads kernel)
 	const int tail_c = A.nt4 ? -1 : ((len & 15) ? (len >> 4) : -1);
+	const int tail_r = len & 15;
 	const int nt4m = -(int)A.nt4;   // 0 or -1 (the host stores 0 / 1); kept arithmetic so
 	                                  // the test stays one compare, not (c == tail_c) || nt4
 
@@ -1017,7 +1059,7 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	if constexpr (PEEL) {
 		if (nit > 0 && (A.variant & 1u) == 0) {
 			quad_fix(d1, w1, w2, w3, w4);
-			packed_streams<K, ABL>(A, c_lo, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt);
+			packed_streams<K, ABL>(A, c_lo, tail_c, tail_r, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt);
 			w0 = w4; w1 = w5; w2 = w6; w3 = w7; w4 = w8; d1 = d5;
 			w5 = x5; w6 = x6; w7 = x7; w8 = x8; d5 = d9;
 			wi += 4;
@@ -1055,8 +1097,8 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 		}
 		quad_fix(d1, w1, w2, w3, w4);
 		quad_fix(d5, w5, w6, w7, w8);
-		packed_chunk<K, ABL, J0>(A, c, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q, tl, lane);
-		packed_chunk<K, ABL>(A, c + 1, tail_c, nt4m, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q, tl, lane);
+		packed_chunk<K, ABL, J0>(A, c, tail_c, tail_r, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q, tl, lane);
+		packed_chunk<K, ABL>(A, c + 1, tail_c, tail_r, nt4m, sh, w4, w5, w6, w7, w8, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q, tl, lane);
 		w0 = w8;
 		w1 = n0; w2 = n1; w3 = n2; w4 = n3; d1 = dn0;
 		w5 = n4; w6 = n5; w7 = n6; w8 = n7; d5 = dn4;
@@ -1078,7 +1120,7 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 		quad_fix(d5, w5, w6, w7, w8);
 		const bool pair = it + 1 < nit;
 		if (pair)
-			packed_chunk<K, ABL>(A, c_lo + it, tail_c, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q,
+			packed_chunk<K, ABL>(A, c_lo + it, tail_c, tail_r, nt4m, sh, w0, w1, w2, w3, w4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q,
 			                     tl, lane);
 		// the wave's last chunk: windows j end at 16 cl + j and are valid only
 		// below vhi, so when no lane has more than 8 of them (150-bp reads: 6)
@@ -1087,10 +1129,10 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 		const uint32_t x0 = pair ? w4 : w0, x1 = pair ? w5 : w1, x2 = pair ? w6 : w2, x3 = pair ? w7 : w3,
 		               x4 = pair ? w8 : w4;
 		if ((A.variant & 4u) == 0 && __ballot(vhi - 16 * cl > 8) == 0)
-			packed_chunk<K, ABL, 0, 8>(A, cl, tail_c, nt4m, sh, x0, x1, x2, x3, x4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q, tl,
+			packed_chunk<K, ABL, 0, 8>(A, cl, tail_c, tail_r, nt4m, sh, x0, x1, x2, x3, x4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q, tl,
 			                           lane);
 		else
-			packed_chunk<K, ABL>(A, cl, tail_c, nt4m, sh, x0, x1, x2, x3, x4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q, tl,
+			packed_chunk<K, ABL>(A, cl, tail_c, tail_r, nt4m, sh, x0, x1, x2, x3, x4, Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q, tl,
 			                     lane);
 	}
 }
@@ -1112,6 +1154,7 @@ __device__ __forceinline__ void scan_span_quad(const VcKernelArgs &A, const uint
 {
 	if (nit == 0) return;            // wave-uniform; the loads below assume a chunk
 	const int tail_c = A.nt4 ? -1 : ((len & 15) ? (len >> 4) : -1);
+	const int tail_r = len & 15;
 	const int nt4m = -(int)A.nt4;
 	const uint64_t addr = off + 16ull * (uint64_t)c_lo;
 	uint64_t wi = addr >> 2;
@@ -1133,7 +1176,7 @@ __device__ __forceinline__ void scan_span_quad(const VcKernelArgs &A, const uint
 	if constexpr (PEEL) {
 		if ((A.variant & 1u) == 0) {
 			quad_fix(d[0], w[1], w[2], w[3], w[4]);
-			packed_streams<K, ABL>(A, c_lo, tail_c, nt4m, sh, w[0], w[1], w[2], w[3], w[4], Bm1, Bm2, Cm1, Cm2, U, Qe, H,
+			packed_streams<K, ABL>(A, c_lo, tail_c, tail_r, nt4m, sh, w[0], w[1], w[2], w[3], w[4], Bm1, Bm2, Cm1, Cm2, U, Qe, H,
 			                       filt);
 #pragma unroll
 			for (int i = 0; i < 13; ++i) w[i] = w[i + 4];
@@ -1148,12 +1191,12 @@ __device__ __forceinline__ void scan_span_quad(const VcKernelArgs &A, const uint
 	}
 	auto chunk = [&](auto j0tag, auto j1tag, int c, int b) {
 		packed_chunk<K, ABL, decltype(j0tag)::value, decltype(j1tag)::value>(
-			A, c, tail_c, nt4m, sh, w[b], w[b + 1], w[b + 2], w[b + 3], w[b + 4], Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q,
+			A, c, tail_c, tail_r, nt4m, sh, w[b], w[b + 1], w[b + 2], w[b + 3], w[b + 4], Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q,
 			tl, lane);
 	};
 	auto dchunk = [&](auto j0tag, int c, int b) -> uint32_t {
 		return packed_chunk<K, ABL, decltype(j0tag)::value, 16, true>(
-			A, c, tail_c, nt4m, sh, w[b], w[b + 1], w[b + 2], w[b + 3], w[b + 4], Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q,
+			A, c, tail_c, tail_r, nt4m, sh, w[b], w[b + 1], w[b + 2], w[b + 3], w[b + 4], Bm1, Bm2, Cm1, Cm2, U, Qe, H, filt, Q,
 			tl, lane);
 	};
 	auto trip = [&](auto j0tag) {

@@ -151,6 +151,32 @@ def test_prefilter_modes_vs_oracle(k, filt):
     assert int(want.sum()) > 200
 
 
+@pytest.mark.parametrize("filt", ["bloom", "flank"])
+@pytest.mark.parametrize("k", [16, 21, 31])
+def test_tail_bytes_vs_oracle(k, filt):
+    """Reads of ACGT whose last bytes (the tail chunk: len & 15 of them, every
+    value 1..15, which the kernels decode with seq_nt4_table) come from the
+    odd alphabet: lower case, U, N, other letters, bytes 0..3 (which map to
+    themselves) and bytes >= 0x80; whole waves of tails at once."""
+    rng = np.random.default_rng(900 + k)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    reads = []
+    for i in range(6000):
+        L = int(16 * rng.integers(1, 12) + 1 + i % 15) if i % 7 else int(rng.integers(1, 200))
+        r = acgt[rng.integers(0, 4, L)]
+        t = L & 15
+        odd = ALPHABET[rng.integers(0, ALPHABET.size, t)]
+        keep = rng.random(t) < 0.7
+        r[L - t:] = np.where(keep, r[L - t:], odd)
+        reads.append(r.tobytes())
+    keys, vals, n_pat = table_from_reads(k, reads, rng, n_pat=3000)
+    got, km = gpu_counts(k, keys, vals, n_pat, reads, blocks=2, env={"VAFC_FILTER": filt})
+    want, km_want = oracle_counts(k, keys, vals, n_pat, reads)
+    assert km == km_want
+    assert np.array_equal(got, want)
+    assert int(want.sum()) > 1000
+
+
 @pytest.mark.parametrize("k", [21, 31])
 def test_every_kmer_of_golden_reads_flank(k):
     """The flank bitmap forced on with a dense key set (every k-mer of the golden
