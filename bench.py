@@ -625,10 +625,10 @@ def main():
                 "traffic": traffic,
                 "kernel": "vc_count_reads_kernel (+ vc_count_long_kernel, empty here)",
                 "limiter": "the roofline is HBM (integer byte work, no MFMA); the kernel runs below it, "
-                           "bound by VALU issue: 10.4 VALU per base (about 156 per 16-base chunk-wave, 66 of "
-                           "them the flank lookups) at ~3.85 cycles each is ~0.75 of the kernel time; HBM "
-                           "requests are 1.58x the algorithmic bytes at 128 B each (traffic), not the limit; "
-                           "DESIGN.md section 3.1 round 3 and 3.1.1, profiles/r03_final_c2_pmc_counters.json",
+                           "bound by VALU issue: 9.9 VALU per base (about 150 per 16-base chunk-wave, 66 of "
+                           "them the flank lookups) at ~4 cycles each is ~0.8 of the kernel time; HBM "
+                           "requests are 1.43x the algorithmic bytes at 128 B each (traffic), not the limit; "
+                           "DESIGN.md section 3.1 round 3 and 3.1.1, profiles/r03_close2_c2_pmc_counters.json",
                 "kernel_ms": round(k_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
             },
