@@ -408,6 +408,19 @@ inline void copy_match8(uint8_t *dst, unsigned dist, unsigned len)
 // One Huffman-coded block body up to its end-of-block code.  Returns 1 at
 // the end of the block, 0 on an error, 2 (phase 1 only) when the output has
 // just switched to phase 2 and the block continues there.
+//
+// Phase 1, a match whose source is output (src >= 0) at distance >= 8: the
+// first 16 symbols are copied unconditionally (two 16-byte moves; longer
+// matches continue 8 at a time) and ORed to see whether a marker came along.
+// Level-1 FASTQ is almost all matches (8 symbols on average, 85 % of them
+// from a source that may hold markers: profiles/r03_gz_symbols.log), and the
+// branches on the length and on the source's markers were the loop's
+// unpredictable ones: +12 % on one thread of the box
+// (profiles/r03_gz_ab_cp16.log).  The look may see up to 15 symbols past the
+// source range, all of them output already: it can only move last_mark up,
+// which is safe (it delays phase 2).  The same loop with the reader and the
+// cursor in locals was 12 % slower on the box
+// (profiles/r03_gz_ab_decoder_locals.log).
 template <bool WIDE>
 int decode_huff(BitIn &in, const Tables &T, Out &o)
 {
@@ -469,35 +482,38 @@ int decode_huff(BitIn &in, const Tables &T, Out &o)
 		}
 		const int64_t src = (int64_t)o.ns - (int64_t)dist;
 		uint16_t *dst = o.s + o.ns;
-		if (src >= 0) {
-			const uint16_t *s = dst - dist;
-			if (src <= o.last_mark) {   // the source may hold markers: copy and look
-				uint64_t acc = 0;
-				if (dist >= 8) {   // (the look may see up to 7 symbols past the source: harmless)
-					for (unsigned i = 0; i < len; i += 8) {
-						uint64_t a, b;
-						memcpy(&a, s + i, 8);
-						memcpy(&b, s + i + 4, 8);
-						memcpy(dst + i, &a, 8);
-						memcpy(dst + i + 4, &b, 8);
-						acc |= a | b;
-					}
-				} else {
-					for (unsigned i = 0; i < len; ++i) {
-						const uint16_t v = s[i];
-						dst[i] = v;
-						acc |= v;
-					}
-				}
-				if (acc & 0x8000800080008000ull) o.last_mark = (int64_t)o.ns + len - 1;
-			} else if (dist >= 8) {
-				for (unsigned i = 0; i < len; i += 8) memcpy(dst + i, s + i, 16);
-			} else if (dist == 1) {
-				const uint16_t v = s[0];
-				for (unsigned i = 0; i < len; ++i) dst[i] = v;
-			} else {
-				for (unsigned i = 0; i < len; ++i) dst[i] = s[i];
+		if (__builtin_expect(src >= 0 && dist >= 8, 1)) {
+			// 8 symbols per step, in order, each from a source that ends
+			// before the step's destination starts (dist >= 8)
+			const uint16_t *q = dst - dist;
+			uint64_t a, b, c, f;
+			memcpy(&a, q, 8);
+			memcpy(&b, q + 4, 8);
+			memcpy(dst, &a, 8);
+			memcpy(dst + 4, &b, 8);
+			memcpy(&c, q + 8, 8);
+			memcpy(&f, q + 12, 8);
+			memcpy(dst + 8, &c, 8);
+			memcpy(dst + 12, &f, 8);
+			uint64_t acc = a | b | c | f;
+			for (unsigned i = 16; i < len; i += 8) {
+				memcpy(&a, q + i, 8);
+				memcpy(&b, q + i + 4, 8);
+				memcpy(dst + i, &a, 8);
+				memcpy(dst + i + 4, &b, 8);
+				acc |= a | b;
 			}
+			const int64_t lm = (int64_t)o.ns + len - 1;
+			o.last_mark = (acc & 0x8000800080008000ull) ? lm : o.last_mark;
+		} else if (src >= 0) {
+			const uint16_t *q = dst - dist;
+			uint16_t acc = 0;
+			for (unsigned i = 0; i < len; ++i) {
+				const uint16_t v = q[i];
+				dst[i] = v;
+				acc |= v;
+			}
+			if (acc & MARK) o.last_mark = (int64_t)o.ns + len - 1;
 		} else {
 			if (src < o.floor) return 0;   // before the member's first byte
 			const uint32_t m = (uint32_t)(src + WSIZE);
