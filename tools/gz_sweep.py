@@ -34,7 +34,7 @@ def main():
     import vafc_synth as S
     dev = torch.device("cuda", 0)
     panel = S.grch38_panel()
-    tmp = tempfile.mkdtemp(prefix="gzsweep_")
+    tmp = bench.scratch_dir(args.reads * 330 * 1.3, tempfile.mkdtemp(prefix="gzsweep_"))   # /dev/shm when it fits
     pat = os.path.join(tmp, "p.txt")
     panel.write_patterns(pat, 21)
     R, L = args.reads, 150
@@ -54,6 +54,7 @@ def main():
     del d_seq, d_offs, d_lens
     print("file: %d reads, %.2f GB text, %.2f GB gzip" % (R, os.path.getsize(fq) / 1e9, os.path.getsize(gz) / 1e9),
           flush=True)
+    os.unlink(fq)
     for v in [x.strip() for x in args.variants.split(";") if x.strip()]:
         env = dict(os.environ, **dict(kv.split("=", 1) for kv in v.split()))
         rs = [bench.cli_run(bench.PRODUCT_CLI, pat, gz, args.threads, os.path.join(tmp, "o.vaf"), 21, env=env)
