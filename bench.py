@@ -243,7 +243,9 @@ def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None, dev=None, device_
         runs = []
         for rep in range(3):
             o = os.path.join(tmp, "e2e_%s.vaf" % name)
-            r = cli_run(PRODUCT_CLI, pat, path, t, o, k, env=env)
+            # a run takes seconds; a hang (e.g. in a multi-GPU RCCL set-up) ends the
+            # leg after 3 minutes instead of holding the whole bench line back
+            r = cli_run(PRODUCT_CLI, pat, path, t, o, k, env=env, timeout=180)
             runs.append(r)
             log("e2e %s -t %d (run %d): %.1f Mbases/s counting phase, %.2fs process" %
                 (name, t, rep + 1, r["mbases"], r["wall"]))
