@@ -99,8 +99,11 @@ struct BitIn {
 };
 
 // ---------------------------------------------------------------------------
-// Huffman decoding tables.  Entry: bits 0-7 code length to consume, 8-12 extra
-// bits (or sub-table index bits), 13-15 kind, 16-31 value.
+// Huffman decoding tables.  Entry: bits 0-7 bits to consume, 8-12 extra bits
+// (or sub-table index bits), 13-15 kind, 16-31 value.  A length or distance
+// entry consumes its code AND its extra bits in one shift; the extra bits are
+// read from the bit buffer before it (at the code length, bits - extra), so
+// the next table lookup waits for one shift instead of two.
 // ---------------------------------------------------------------------------
 // K_LIT2: two literals in one literal/length table entry (value = first |
 // second << 8, length = both codes): DNA literals have 2-3-bit codes, so most
@@ -135,10 +138,10 @@ inline uint32_t sym_entry(Code c, unsigned s, unsigned len)
 	if (c == C_LIT) {
 		if (s < 256) return mk(len, 0, K_LIT, s);
 		if (s == 256) return mk(len, 0, K_EOB, 0);
-		if (s <= 285) return mk(len, LEXT[s - 257], K_LEN, LBASE[s - 257]);
+		if (s <= 285) return mk(len + LEXT[s - 257], LEXT[s - 257], K_LEN, LBASE[s - 257]);   // length: code + extra bits
 		return mk(len, 0, K_BAD, 0);
 	}
-	if (c == C_DIST) return s < 30 ? mk(len, DEXT[s], K_LIT, DBASE[s]) : mk(len, 0, K_BAD, 0);
+	if (c == C_DIST) return s < 30 ? mk(len + DEXT[s], DEXT[s], K_LIT, DBASE[s]) : mk(len, 0, K_BAD, 0);
 	return mk(len, 0, K_LIT, s);
 }
 
@@ -435,6 +438,7 @@ int decode_huff(BitIn &in, const Tables &T, Out &o)
 		in.refill();
 		uint32_t e = T.lit[in.buf & ((1u << LROOT) - 1)];
 		if (e_kind(e) == K_SUB) e = T.lit[e_val(e) + ((in.buf >> LROOT) & ((1u << e_ext(e)) - 1))];
+		const uint64_t b0 = in.buf;   // a length's extra bits are read from here
 		in.drop(e_len(e));
 		if (e_kind(e) <= K_LIT2) {
 			// one or two literals per entry, written as a pair (the second
@@ -468,12 +472,15 @@ int decode_huff(BitIn &in, const Tables &T, Out &o)
 		}
 		if (e_kind(e) == K_EOB) return in.overrun() ? 0 : 1;
 		if (e_kind(e) != K_LEN) return 0;
-		const unsigned len = e_val(e) + in.take(e_ext(e));
+		const unsigned lx = e_ext(e);
+		const unsigned len = e_val(e) + (unsigned)((b0 >> (e_len(e) - lx)) & ((1u << lx) - 1));
 		uint32_t d = T.dist[in.buf & ((1u << DROOT) - 1)];
 		if (e_kind(d) == K_SUB) d = T.dist[e_val(d) + ((in.buf >> DROOT) & ((1u << e_ext(d)) - 1))];
 		if (e_kind(d) == K_BAD) return 0;
+		const uint64_t b1 = in.buf;
 		in.drop(e_len(d));
-		const unsigned dist = e_val(d) + in.take(e_ext(d));
+		const unsigned dx = e_ext(d);
+		const unsigned dist = e_val(d) + (unsigned)((b1 >> (e_len(d) - dx)) & ((1u << dx) - 1));
 		if (!WIDE) {   // every source byte lies in t[nt - 32768, nt): literal text
 			if ((int64_t)o.nt - (int64_t)dist < o.floor) return 0;
 			copy_match8(o.t + o.nt, dist, len);
@@ -574,6 +581,7 @@ int decode_huff_narrow(BitIn &in, const Tables &T, Out &o)
 		}
 		uint32_t e = LT[buf & ((1u << LROOT) - 1)];
 		if (e_kind(e) == K_SUB) e = LT[e_val(e) + ((buf >> LROOT) & ((1u << e_ext(e)) - 1))];
+		const uint64_t b0 = buf;   // a length's extra bits are read from here
 		buf >>= e_len(e);
 		cnt -= e_len(e);
 		if (e_kind(e) <= K_LIT2) {   // see decode_huff
@@ -601,21 +609,18 @@ int decode_huff_narrow(BitIn &in, const Tables &T, Out &o)
 			return 0;
 		}
 		const unsigned lx = e_ext(e);
-		const unsigned len = e_val(e) + (unsigned)(buf & ((1ull << lx) - 1));
-		buf >>= lx;
-		cnt -= lx;
+		const unsigned len = e_val(e) + (unsigned)((b0 >> (e_len(e) - lx)) & ((1u << lx) - 1));
 		uint32_t d = DT[buf & ((1u << DROOT) - 1)];
 		if (e_kind(d) == K_SUB) d = DT[e_val(d) + ((buf >> DROOT) & ((1u << e_ext(d)) - 1))];
 		if (e_kind(d) == K_BAD) {
 			save();
 			return 0;
 		}
+		const uint64_t b1 = buf;
 		buf >>= e_len(d);
 		cnt -= e_len(d);
 		const unsigned dx = e_ext(d);
-		const unsigned dist = e_val(d) + (unsigned)(buf & ((1ull << dx) - 1));
-		buf >>= dx;
-		cnt -= dx;
+		const unsigned dist = e_val(d) + (unsigned)((b1 >> (e_len(d) - dx)) & ((1u << dx) - 1));
 		// every source byte lies in t[nt - 32768, nt): literal text
 		if (__builtin_expect((int64_t)nt - (int64_t)dist < floor, 0)) {
 			save();

@@ -25,7 +25,8 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--scaling", default="", help="also time the inflater alone at these thread counts")
     ap.add_argument("--variants", default="", help="';'-separated groups of space-separated KEY=VAL env "
-                                                   "settings, each timed with the CLI (instead of --parsers)")
+                                                   "settings, each timed with the CLI (instead of --parsers); "
+                                                   "CLI=path runs another vaf-counter build")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -57,7 +58,8 @@ def main():
     os.unlink(fq)
     for v in [x.strip() for x in args.variants.split(";") if x.strip()]:
         env = dict(os.environ, **dict(kv.split("=", 1) for kv in v.split()))
-        rs = [bench.cli_run(bench.PRODUCT_CLI, pat, gz, args.threads, os.path.join(tmp, "o.vaf"), 21, env=env)
+        cli = os.path.abspath(env.pop("CLI", bench.PRODUCT_CLI))   # CLI=path: another build (A/B)
+        rs = [bench.cli_run(cli, pat, gz, args.threads, os.path.join(tmp, "o.vaf"), 21, env=env)
               for _ in range(args.reps)]
         print("%-60s CLI %s Mbases/s (process %s s)" % (v, [round(r["mbases"]) for r in rs],
                                                         [round(r["wall"], 2) for r in rs]), flush=True)
