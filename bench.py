@@ -73,6 +73,24 @@ def cpu_share(gpus=1):
     return max(1, min(16 * gpus, n))
 
 
+# What bounds the counting kernel below its HBM roofline (PMC of the closing
+# kernels).  Panels of more than 65,536 keys take the
+# large-panel path (LDS Bloom filter + L2 second-level filter).
+LIMITER_FLANK = ("the roofline is HBM (integer byte work, no MFMA); the kernel runs below it, bound by VALU "
+                 "issue: 9.9 VALU per base (about 150 per 16-base chunk-wave, 66 of them the flank lookups) at "
+                 "~4 cycles each is ~0.8 of the kernel time, the LDS array busy ~0.58 of it (70 % of that bank "
+                 "conflicts of the random lookups); HBM requests are 1.43x the algorithmic bytes at 128 B each "
+                 "(traffic), not the limit; DESIGN.md section 3.1 round 3 and 3.1.1, "
+                 "profiles/r03_close2_c2_pmc_counters.json")
+LIMITER_LARGE_PANEL = ("the roofline is HBM (integer byte work, no MFMA); the large-panel kernel runs far below "
+                       "it, bound by VALU issue and the texture-address (TA) rate of its gathers: 9.3 % of "
+                       "windows pass the 144 KiB LDS Bloom filter (about 6 % is that size's information limit "
+                       "for 200k SNP pairs), each pass is a hit-loop trip and one lane of a random gather into "
+                       "the L2-resident second-level filter; 23.6 VALU per base (5.5 G per launch, ~0.8 of the "
+                       "kernel time at ~4 cycles each), TA busy ~0.5 of the cycles; DESIGN.md section 3.1 "
+                       "(large panels), profiles/r03_close2_c5_pmc_counters.json")
+
+
 def cli_run(binary, pat, fq, threads, out, k, env=None, timeout=900):
     """A vaf-counter CLI (reference or drop-in) with -v: its own counting-phase
     Speed line (bases / counting wall clock, vaf-counter.c:707) and k-mer rate."""
@@ -626,11 +644,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel": "vc_count_reads_kernel (+ vc_count_long_kernel, empty here)",
-                "limiter": "the roofline is HBM (integer byte work, no MFMA); the kernel runs below it, "
-                           "bound by VALU issue: 9.9 VALU per base (about 150 per 16-base chunk-wave, 66 of "
-                           "them the flank lookups) at ~4 cycles each is ~0.8 of the kernel time; HBM "
-                           "requests are 1.43x the algorithmic bytes at 128 B each (traffic), not the limit; "
-                           "DESIGN.md section 3.1 round 3 and 3.1.1, profiles/r03_close2_c2_pmc_counters.json",
+                "limiter": (LIMITER_LARGE_PANEL if tinfo["n_keys"] > 65536 else LIMITER_FLANK),
                 "kernel_ms": round(k_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
             },
