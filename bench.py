@@ -386,12 +386,11 @@ def main():
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    # Every torch op and every vafc launch of this process on one real stream:
-    # torch's default stream has the handle 0, which vc_count_device reads as
-    # "the counter's own stream" (non-blocking, no order with torch's work), so
-    # a zero-fill or a read generation on the default stream would race with
-    # the counting kernel.
-    torch.cuda.set_stream(torch.cuda.Stream(device=dev))
+    # Every torch op and every vafc launch of this process run on torch's
+    # default stream: its handle 0 is HIP's null stream, which vc_count_device
+    # takes as such (include/vafc.h; the round-3 ABI read 0 as the counter's
+    # own stream, and a zero-fill on torch's default stream raced with the
+    # count, profiles/r03_rank1_parity_race.log).
     if world > 1:
         backend = os.environ.get("VAFC_DIST_BACKEND", "nccl")
         if backend == "nccl":

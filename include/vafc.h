@@ -104,9 +104,17 @@ void vc_destroy(vc_ctx *ctx);
 int vc_count_block(vc_ctx *ctx, const uint8_t *seq, size_t seq_bytes,
                    const uint64_t *offs, const uint32_t *lens, uint64_t n_reads);
 
+/* The counter's own (non-blocking) stream as vc_count_device's `stream`. */
+#define VC_STREAM_CTX ((void *)(intptr_t)-1)
+
 /* Same for device-resident reads (HBM pointers, e.g. from torch or
- * hipMalloc); enqueued on `stream` (a hipStream_t, NULL = the ctx stream).
- * No host synchronisation.  seq_bytes bounds every device read. */
+ * hipMalloc); enqueued on `stream`, a hipStream_t: NULL is HIP's null stream,
+ * ordered with the legacy default stream (torch's default stream) as for any
+ * HIP API; VC_STREAM_CTX is the counter's own stream (vc_stream).  Whatever
+ * the stream, the launch is ordered after the counter's earlier work on its
+ * own stream (vc_reset, earlier batches) and before its later work (vc_finish,
+ * the shard sum), so vc_finish needs no device-wide synchronisation.  No host
+ * synchronisation.  seq_bytes bounds every device read. */
 int vc_count_device(vc_ctx *ctx, const uint8_t *d_seq, size_t seq_bytes,
                     const uint64_t *d_offs, const uint32_t *d_lens, uint64_t n_reads,
                     void *stream);
@@ -188,7 +196,8 @@ typedef struct {
  * are streamed to the device in large pinned batches.  Plain (uncompressed)
  * files of 32 MB or more are parsed by n_threads worker threads (the CLI's
  * -t; vafc_ingest.h) with identical results; gzip files are inflated by
- * n_threads workers (vafc_gzip.h, gzread's output) and parsed by one thread;
+ * n_threads workers (vafc_gzip.h, gzread's output) while (n_threads + 3) / 5
+ * workers parse the inflated text in parallel (VAFC_GZ_PARSERS overrides);
  * small plain files use one reader thread.  Returns VC_EIO if the file cannot be opened (the reference
  * skips such files silently, vaf-counter.c:557). */
 int vc_count_file(vc_ctx *ctx, const char *path, int block_bases, int n_threads,

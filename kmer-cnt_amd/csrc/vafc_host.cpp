@@ -268,6 +268,10 @@ struct vc_ctx {
 	std::vector<Slot> islot;               // parallel ingest (vc_count_file on plain files)
 	bool timing = false, timed = false;
 	hipEvent_t t0 = nullptr, t1 = nullptr;
+	// vc_count_device on a stream other than st: st's work so far -> that
+	// stream (ev_in), and the launch -> st (ev_out), so that vc_reset, vc_finish
+	// and the shard sum, all on st, stay ordered with it (created on first use)
+	hipEvent_t ev_in = nullptr, ev_out = nullptr;
 	struct Kc *kc = nullptr;               // histogram mode (vc_kc_create)
 	// multi-GPU (vc_create_multi): this ctx is shard 0; rep[i - 1] is shard i
 	std::vector<vc_ctx *> rep;
@@ -498,6 +502,8 @@ extern "C" void vc_destroy(vc_ctx *c)
 	}
 	if (c->t0) (void)hipEventDestroy(c->t0);
 	if (c->t1) (void)hipEventDestroy(c->t1);
+	if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+	if (c->ev_out) (void)hipEventDestroy(c->ev_out);
 	if (c->d_table) (void)hipFree(c->d_table);
 	if (c->d_filter) (void)hipFree(c->d_filter);
 	if (c->d_l2f) (void)hipFree(c->d_l2f);
@@ -657,8 +663,20 @@ extern "C" int vc_count_device(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes
 		++c->batches;
 	}
 	HIPCK(hipSetDevice(c->dev));
-	return launch(c, d_seq, seq_bytes, d_offs, d_lens, n_reads,
-	              stream ? (hipStream_t)stream : c->st);
+	// NULL is HIP's null stream (ordered with the legacy default stream, which
+	// is torch's default stream), as for every HIP API; VC_STREAM_CTX is the
+	// counter's own non-blocking stream
+	const hipStream_t st = stream == VC_STREAM_CTX ? c->st : (hipStream_t)stream;
+	if (st == c->st) return launch(c, d_seq, seq_bytes, d_offs, d_lens, n_reads, st);
+	if (!c->ev_in) HIPCK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
+	if (!c->ev_out) HIPCK(hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming));
+	HIPCK(hipEventRecord(c->ev_in, c->st));           // e.g. a vc_reset before this call
+	HIPCK(hipStreamWaitEvent(st, c->ev_in, 0));
+	const int rc = launch(c, d_seq, seq_bytes, d_offs, d_lens, n_reads, st);
+	if (rc != VC_OK) return rc;
+	HIPCK(hipEventRecord(c->ev_out, st));
+	HIPCK(hipStreamWaitEvent(c->st, c->ev_out, 0));   // vc_finish waits on c->st only
+	return VC_OK;
 }
 
 static int slot_reserve(Slot &s, size_t bytes, size_t reads)
@@ -738,9 +756,10 @@ extern "C" int vc_finish(vc_ctx *c, uint32_t *counts, uint64_t *kmers)
 			vc_ctx *sh = shard_at(c, i);
 			uint32_t f = 0;
 			HIPCK(hipSetDevice(sh->dev));
-			// the whole device: vc_count_device may have launched on a caller
-			// stream that does not synchronise with the shard's own
-			HIPCK(hipDeviceSynchronize());
+			// the shard's stream also waits for its launches on caller
+			// streams (vc_count_device), so this covers every batch without
+			// waiting on the caller's unrelated work on the device
+			HIPCK(hipStreamSynchronize(sh->st));
 			HIPCK(hipMemcpy(&f, sh->d_flags, sizeof f, hipMemcpyDeviceToHost));
 			if (f & 1u) {
 				fprintf(stderr, "[E::vafc] more reads longer than %d bases than the long-read list holds "
@@ -754,7 +773,6 @@ extern "C" int vc_finish(vc_ctx *c, uint32_t *counts, uint64_t *kmers)
 	}
 	HIPCK(hipSetDevice(c->dev));
 	HIPCK(hipStreamSynchronize(c->st));
-	HIPCK(hipDeviceSynchronize());
 	for (auto &s : c->slot) s.pending = false;
 	if (c->kc) {   // histogram mode: the k-mers seen (vc_kc_histogram gives the rest)
 		if (kmers) {

@@ -1024,7 +1024,9 @@ __device__ __forceinline__ void scan_span_packed(const VcKernelArgs &A, const ui
 	// in seq_nt4 mode (snp-pattern-gen) every chunk does: tail_c = -1 and the
 	// test (c | -1) == -1 always holds (the OR is scalar in the reads kernel)
 	const int tail_c = A.nt4 ? -1 : ((len & 15) ? (len >> 4) : -1);
-	const int tail_r = len & 15;
+	// seq_nt4 mode decodes all 16 bytes of every chunk with the table: every
+	// dword of the chunk holds "tail" bytes (dec_tail_chunk tests tail_r)
+	const int tail_r = A.nt4 ? 16 : (len & 15);
 	const int nt4m = -(int)A.nt4;   // 0 or -1 (the host stores 0 / 1); kept arithmetic so
 	                                  // the test stays one compare, not (c == tail_c) || nt4
 
@@ -1154,7 +1156,9 @@ __device__ __forceinline__ void scan_span_quad(const VcKernelArgs &A, const uint
 {
 	if (nit == 0) return;            // wave-uniform; the loads below assume a chunk
 	const int tail_c = A.nt4 ? -1 : ((len & 15) ? (len >> 4) : -1);
-	const int tail_r = len & 15;
+	// seq_nt4 mode decodes all 16 bytes of every chunk with the table: every
+	// dword of the chunk holds "tail" bytes (dec_tail_chunk tests tail_r)
+	const int tail_r = A.nt4 ? 16 : (len & 15);
 	const int nt4m = -(int)A.nt4;
 	const uint64_t addr = off + 16ull * (uint64_t)c_lo;
 	uint64_t wi = addr >> 2;

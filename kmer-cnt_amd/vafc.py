@@ -28,6 +28,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VAFC_LIB", os.path.join(_HERE, "lib", "libvafc.so"))
 
+# vc_count_device's stream argument for the counter's own stream (VC_STREAM_CTX)
+STREAM_CTX = (1 << 64) - 1
+
 VC_OK, VC_EINVAL, VC_ENOMEM, VC_EHIP, VC_ENODEV, VC_EIO, VC_ETOOMANY, VC_EFULL = 0, -1, -2, -3, -4, -5, -6, -7
 
 # every symbol include/vafc.h declares
@@ -338,6 +341,11 @@ class KmerMap:
 
     def count_device(self, seq_ptr: int, seq_bytes: int, offs_ptr: int, lens_ptr: int,
                      n_reads: int, stream: int = 0) -> None:
+        """Count HBM-resident reads on `stream` (a hipStream_t handle): 0 is HIP's
+        null stream, i.e. torch's default stream, so reads written by torch on
+        its current stream are ordered before the count when that handle is
+        passed (torch.cuda.current_stream().cuda_stream); STREAM_CTX is the
+        counter's own stream."""
         _ck(lib().vc_count_device(self._h, P(seq_ptr), seq_bytes, P(offs_ptr), P(lens_ptr),
                                   n_reads, P(stream) if stream else None), "vc_count_device")
 

@@ -209,6 +209,27 @@ def test_long_reads_segmented_kernel(k):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("filt", [None, "bloom128"])
+@pytest.mark.parametrize("k", [21, 31])
+def test_long_reads_large_panel(k, filt):
+    """Large tables (> 65,536 keys: second-level filter, and for k >= 21 the
+    144 KiB LDS filter with 128-entry queues, VC_KV_BIG) in the segmented
+    long-read kernel, whose segments start mid-read (HAS_LO); VAFC_FILTER=
+    bloom128 keeps the 128 KiB filter."""
+    rng = np.random.default_rng(3100 + k)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    lens = [16385, 65543, 300_000] + list(rng.integers(100, 300, 1200))
+    reads = [acgt[rng.integers(0, 4, int(L))].tobytes() for L in lens]
+    keys, vals, n_pat = table_from_reads(k, reads, rng, n_pat=70_000)
+    assert keys.size > 65_536
+    env = {"VAFC_FILTER": filt} if filt else None
+    got, km = gpu_counts(k, keys, vals, n_pat, reads, blocks=2, env=env)
+    want, km_want = oracle_counts(k, keys, vals, n_pat, reads)
+    assert km == km_want
+    assert np.array_equal(got, want)
+    assert int(want.sum()) > 40_000
+
+
 @pytest.mark.parametrize("k,n_sel", [(16, 65336), (16, 65337), (27, 65337), (31, 90000)])
 def test_second_level_filter_threshold(k, n_sel):
     """Tables of > 65536 keys (VC_L2F_MIN_KEYS) also build the second-level filter;
@@ -460,6 +481,54 @@ def test_full_size_linearity_and_prefix_parity(torch_dev, config):
     seq = d_seq[: n * L].cpu().numpy()
     want, km_want = orc.count_reads(seq, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint32))
     assert p_k == km_want and np.array_equal(p_c, want)
+    m.close()
+
+
+@pytest.mark.parametrize("shards", [1, 2])
+def test_count_device_default_stream_order(torch_dev, shards):
+    """stream = 0 is HIP's null stream, i.e. torch's default stream (the seam
+    of count_fastq_kmers, vaf-counter.c:550, fed from device memory): the
+    counter's outputs are zeroed and the reads generated on torch's default
+    stream behind a long queue of unrelated work, then counted with stream 0
+    and no host synchronisation; vc_finish (which waits on the counter's own
+    stream only) must see exactly the oracle's counts.  Repeated after a
+    vc_reset issued while the next reads are still being written."""
+    import torch
+    import vafc
+    import vafc_synth as S
+    import oracle as O
+    import tempfile
+    assert torch.cuda.current_stream().cuda_stream == 0
+    panel = S.grch38_panel()
+    R, L, k = 1_000_000, 150, 21
+    with tempfile.TemporaryDirectory() as d:
+        pat = os.path.join(d, "p.txt")
+        panel.write_patterns(pat, k)
+        db = vafc.load_patterns(pat)
+        keys, vals, _ = db.keys(k)
+        orc = O.Oracle(k, pattern_fn=pat)
+    m = vafc.KmerMap(k, keys, vals, db.n, 0) if shards == 1 else vafc.KmerMap(k, keys, vals, db.n, devices=[0] * shards)
+    win = torch.from_numpy(panel.windows().reshape(-1)).to(torch_dev)
+    dos = torch.from_numpy(panel.dosage.astype(np.uint8)).to(torch_dev)
+    busy = torch.empty(1 << 30, dtype=torch.uint8, device=torch_dev)
+    torch.cuda.synchronize()
+    for rnd, seed in enumerate((42, 43)):
+        d_seq = torch.empty(R * L, dtype=torch.uint8, device=torch_dev)
+        d_offs = torch.empty(R, dtype=torch.int64, device=torch_dev)
+        d_lens = torch.empty(R, dtype=torch.int32, device=torch_dev)
+        for i in range(40):   # ~40 GB of unrelated writes queued ahead of the reads
+            busy.fill_(i)
+        vafc.synth_reads(d_seq.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), 0, R, L, seed, 0.01,
+                         win.data_ptr(), dos.data_ptr(), panel.n, 0)
+        if rnd:
+            m.reset()
+        for a in range(0, R, R // 4):   # four batches (dealt over the shards)
+            m.count_device(d_seq.data_ptr(), R * L, d_offs.data_ptr() + 8 * a, d_lens.data_ptr() + 4 * a, R // 4)
+        got, km = m.finish()
+        seq = d_seq.cpu().numpy()
+        want, km_want = orc.count_reads(seq, np.arange(R, dtype=np.uint64) * L, np.full(R, L, np.uint32))
+        assert km == km_want and np.array_equal(got, want)
+        assert int(want.astype(np.uint64).sum()) > 1000
     m.close()
 
 

@@ -30,7 +30,7 @@ two_gpus = pytest.mark.skipif("_n_devices() < 2", reason="needs two GPUs")
 # golden cases covering plain/gz input, -b 1, two files, the stop rule, empty input
 SHARDED_CASES = ["c1_plumbing_k21", "c1_plumbing_k21_gz", "c1_k21_b1", "pe_k31", "missing_file",
                  "mal_gbbbgbbbg", "mal_gbbbgbbbg_b1", "mal_bbbg_b1", "edge_k15", "edge_gz", "truncated",
-                 "empty_reads", "empty_patterns"]
+                 "empty_reads", "empty_patterns", "pal_k21", "pal_k16"]
 
 MODES = {
     # sequential reader, 3 kB batches dealt over two shards

@@ -157,6 +157,60 @@ def test_count_candidates_random_genome(k):
     assert int(want.sum()) > 1000
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [21, 31, 17])
+def test_count_candidates_long_odd_alphabet(k):
+    """Chromosomes over 16,384 bases (the segmented kernel, every lane the same
+    length) with len % 16 in {0, 4, 12} and bytes that the reference's PSHUFB
+    head decode accepts but seq_nt4_table rejects (S/W/D/E/Q either case,
+    bytes 4..7): in seq_nt4 mode all 16 bytes of every chunk take the table
+    (snp-pattern-gen.c:39-56,159-190)."""
+    import vafc
+    import oracle as O
+    rng = np.random.default_rng(70 + k)
+    odd = np.frombuffer(b"SWDEQswdeq\x04\x05\x06\x07Nn", np.uint8)
+    seqs = []
+    for L in (16_400, 20_004, 30_012, 65_536 + 12):
+        s = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, L)].copy()
+        pos = rng.integers(0, L, L // 200)
+        s[pos] = odd[rng.integers(0, odd.size, pos.size)]
+        seqs.append(s.tobytes())
+    assert all(len(s) % 16 in (0, 4, 12) and len(s) > 16384 for s in seqs)
+    # keys: canonical k-mers of the table decode, plus k-mers that occur only
+    # when the odd bytes take the PSHUFB head decode (vaf-counter's quirk)
+    pool = np.unique(np.concatenate([_nt4_kmers(k, s) for s in seqs]))
+    head = np.unique(np.concatenate([O.read_kmers(k, s) for s in seqs]))
+    fake = np.setdiff1d(head, pool)
+    assert fake.size > 500
+    keys = np.unique(np.concatenate([pool[rng.permutation(pool.size)[:2000]], fake[rng.permutation(fake.size)[:2000]]]))
+    got = vafc.count_candidate_kmers(k, seqs, keys)
+    want = _oracle_counts(k, seqs, keys)
+    assert np.array_equal(got, want)
+    assert int(want.sum()) > 1000
+
+
+def _nt4_kmers(k, s):
+    """Canonical k-mers of s under seq_nt4_table (snp-pattern-gen.c:159-190)."""
+    nt4 = np.full(256, 4, np.int64)
+    for i, ch in enumerate(b"ACGT"):
+        nt4[ch] = nt4[ch + 32] = i
+        nt4[i] = i
+    nt4[ord("U")] = nt4[ord("u")] = 3
+    mask, shift = (1 << (2 * k)) - 1, 2 * (k - 1)
+    out, x0, x1, l = [], 0, 0, 0
+    for b in s:
+        c = int(nt4[b])
+        if c < 4:
+            x0 = ((x0 << 2) | c) & mask
+            x1 = (x1 >> 2) | ((3 - c) << shift)
+            l += 1
+            if l >= k:
+                out.append(min(x0, x1))
+        else:
+            x0 = x1 = l = 0
+    return np.array(out, np.uint64)
+
+
 def _rc(x, k):
     r = 0
     for _ in range(k):
