@@ -1800,7 +1800,7 @@ static hipError_t launch_kw(const VcKernelArgs *A, int grid, int grid_long, hipS
 #endif
 
 template <int K>
-static hipError_t launch_k(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
+static hipError_t launch_k_impl(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
 {
 #ifdef VC_ABLATION
 	if constexpr (K == 21) {
@@ -1823,7 +1823,7 @@ static hipError_t launch_k(const VcKernelArgs *A, int grid, int grid_long, hipSt
 }
 
 template <int K>
-static hipError_t setup_k(int lds)
+static hipError_t setup_k_impl(int lds)
 {
 	hipError_t e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<K>,
 	                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -1858,6 +1858,33 @@ static hipError_t setup_k(int lds)
 	}
 #endif
 	return e;
+}
+
+// Development builds of kernel variants (tools/ab_libs.sh, never the product):
+// -DVC_DEV_ONLY=21 [-DVC_DEV_ONLY2=31] instantiates the packed kernels of
+// those k only (k < 16 keeps the run-time-k kernel), so an A/B library builds
+// in a minute instead of compiling all sixteen; other k fail to launch.
+#ifndef VC_DEV_ONLY2
+#define VC_DEV_ONLY2 VC_DEV_ONLY
+#endif
+template <int K>
+static hipError_t launch_k(const VcKernelArgs *A, int grid, int grid_long, hipStream_t st)
+{
+#ifdef VC_DEV_ONLY
+	if constexpr (K != 0 && K != VC_DEV_ONLY && K != VC_DEV_ONLY2) return hipErrorNotSupported;
+	else
+#endif
+		return launch_k_impl<K>(A, grid, grid_long, st);
+}
+
+template <int K>
+static hipError_t setup_k(int lds)
+{
+#ifdef VC_DEV_ONLY
+	if constexpr (K != 0 && K != VC_DEV_ONLY && K != VC_DEV_ONLY2) return hipSuccess;
+	else
+#endif
+		return setup_k_impl<K>(lds);
 }
 
 #endif
