@@ -122,6 +122,7 @@ int main(int argc, char *argv[])
 	// the reader's pinned buffers are allocated inside the counting timer, as
 	// the reference allocates its per-block buffers inside it (vaf-counter.c:489-503)
 	rc = vc_reserve_file_ingest(ctx, n_thread);
+	const double t_reserved = now_s();
 	if (rc != VC_OK) {
 		fprintf(stderr, "Error: counting failed (%s)\n", vc_strerror(rc));
 		vc_destroy(ctx);
@@ -149,8 +150,17 @@ int main(int argc, char *argv[])
 	}
 	std::vector<uint32_t> counts(2 * (size_t)n + 2, 0);
 	uint64_t kmers = 0;
+	const double t_read = now_s();
 	rc = vc_finish(ctx, counts.data(), &kmers);
 	const double t_count = now_s() - t;
+	// VAFC_PHASES=1: the counting timer split into the reader's buffer
+	// allocation (pinned slots of every shard), the reading and counting of
+	// the files, and vc_finish (the last batches, the shard sum / RCCL reduce
+	// and the copy of the counts to the host)
+	if (getenv("VAFC_PHASES"))
+		fprintf(stderr, "[P::main] shards %d threads %d: reserve %.4f s, read+count %.4f s, finish %.4f s, "
+		        "counting %.4f s\n", (int)devices.size(), n_thread, t_reserved - t, t_read - t_reserved,
+		        now_s() - t_read, t_count);
 	if (rc != VC_OK) {
 		fprintf(stderr, "Error: counting failed (%s)\n", vc_strerror(rc));
 		vc_destroy(ctx);
