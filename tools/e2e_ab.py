@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""End-to-end A/B of drop-in CLI builds or settings on the whole C2 stream
+(tools only).  Writes the workload's reads as FASTQ in /dev/shm (as bench.py's
+e2e leg does), optionally gzip level 1, then runs the variants alternately,
+`--rounds` times each, and prints one JSON object with every run's -v Speed
+line and each variant's min / median / max / spread.
+
+    python tools/e2e_ab.py [--reads N] [--gzip] [--threads 16] [--rounds 5] \\
+        numa=kmer-cnt_amd/lib_ab/numa/vaf-counter nonuma=kmer-cnt_amd/lib_ab/numa/vaf-counter,VAFC_NUMA=0
+
+A variant is NAME=CLI[,KEY=VAL...] (CLI relative to the repository root).
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "kmer-cnt_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=100_000_000)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--gzip", action="store_true")
+    ap.add_argument("variants", nargs="+")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import bench
+    import vafc
+    import vafc_synth as S
+    dev = torch.device("cuda", 0)
+    panel = S.grch38_panel()
+    tmp = tempfile.mkdtemp(prefix="vafc_e2eab_")
+    pat = os.path.join(tmp, "p.txt")
+    panel.write_patterns(pat, 21)
+    R, L = a.reads, 150
+    d_seq = torch.empty(R * L, dtype=torch.uint8, device=dev)
+    d_offs = torch.empty(R, dtype=torch.int64, device=dev)
+    d_lens = torch.empty(R, dtype=torch.int32, device=dev)
+    win = torch.from_numpy(panel.windows().reshape(-1)).to(dev)
+    dos = torch.from_numpy(panel.dosage.astype(np.uint8)).to(dev)
+    vafc.synth_reads(d_seq.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), 0, R, L, S.READ_SEED_R1, 0.01,
+                     win.data_ptr(), dos.data_ptr(), panel.n, 0)
+    torch.cuda.synchronize()
+    work = bench.scratch_dir(R * (2 * L + 16) * 1.25, tmp)
+    fq = os.path.join(work, "c2.fq")
+    bench.write_fastq_from_device(d_seq, R, L, fq, threads=a.threads)
+    del d_seq, d_offs, d_lens
+    torch.cuda.empty_cache()
+    path = fq
+    if a.gzip:
+        path = fq + ".gz"
+        bench.gzip_level1(fq, path, a.threads)
+        os.unlink(fq)
+    specs = []
+    for v in a.variants:
+        name, rest = v.split("=", 1)
+        parts = rest.split(",")
+        env = dict(os.environ)
+        for kv in parts[1:]:
+            k_, val = kv.split("=", 1)
+            env[k_] = val
+        specs.append((name, os.path.join(ROOT, parts[0]), env))
+    out = {"workload": "%dM x %d bp reads of the C2 stream, %s, -t %d" % (
+        R // 1_000_000, L, "gzip level 1" if a.gzip else "plain FASTQ", a.threads), "runs": {}}
+    md5s = {}
+    for rep in range(a.rounds):
+        for name, cli, env in specs:
+            o = os.path.join(tmp, name + ".vaf")
+            r = bench.cli_run(cli, pat, path, a.threads, o, 21, env=env, timeout=300)
+            out["runs"].setdefault(name, []).append(r["mbases"])
+            md5s[name] = bench.md5(o)
+            sys.stderr.write("[e2e_ab] %s round %d: %.1f Mbases/s\n" % (name, rep + 1, r["mbases"]))
+    for name, xs in out["runs"].items():
+        s = sorted(xs)
+        med = s[len(s) // 2]
+        out[name] = {"min": s[0], "median": med, "max": s[-1], "spread": round((s[-1] - s[0]) / med, 3)}
+    out["vaf_identical"] = len(set(md5s.values())) == 1
+    print(json.dumps(out))
+    os.unlink(path)
+    if work != tmp:
+        shutil.rmtree(work, ignore_errors=True)
+    shutil.rmtree(tmp, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
