@@ -128,3 +128,105 @@ def test_cli_option_parsing_mirror():
     o, files = vafc.parse_args(["-p", "p", "-o", "o", "--", "-weird.fq"])
     assert files == ["-weird.fq"]
     assert vafc.main(["-p", "p.txt"]) == 1                      # usage -> exit 1
+
+
+# --------------------------------------------------------------------------
+# the torchrun driver (kmer-cnt_amd/vafc_dist.py): files dealt over the ranks,
+# one all-reduce, rank 0 writes the .vaf -- against the reference's goldens
+# --------------------------------------------------------------------------
+
+DIST_CASES = ["pe_k31", "c1_plumbing_k21", "missing_file", "mal_gbbbgbbbg_b1", "pal_k16"]
+
+
+def _driver_rank(rank, world, port, argv, cwd, out_json, counter):
+    import json
+    import sys
+    import torch.distributed as dist
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "kmer-cnt_amd"))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "oracle"))
+    import vafc_dist as D
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    os.chdir(cwd)
+    lines = []
+
+    class OracleRankCounter(D.RankCounter):     # CPU stand-in for the per-GPU counter (test infrastructure)
+        def __init__(self, db, k):
+            import oracle as O
+            self.n = db.n
+            self.orc = O.Oracle(k, pattern_fn=argv[argv.index("-p") + 1])
+            self.counts = np.zeros(2 * db.n + 2, np.uint32)
+            self.km = 0
+
+        def count_file(self, fn, block, threads):
+            rc, b, s, km = self.orc.count_file(fn, block, self.counts)
+            if rc != 0:
+                return False, 0, 0
+            self.km += km
+            return True, b, s
+
+        def local_counts(self):
+            return D.counts_to_tensor(self.counts[:2 * self.n]), self.km
+
+    def make(db, k):
+        if counter == "hip":
+            return D.HipRankCounter(db, k, 0, "gloo")
+        return OracleRankCounter(db, k)
+
+    rc = D.run(argv, make, rank, world, err=lines.append)
+    with open(out_json + ".%d" % rank, "w") as f:
+        json.dump({"rc": rc, "stderr": "".join(lines)}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_driver(entry, synth_dir, tmp_path, counter, world=2):
+    import json
+    import socket
+    import torch.multiprocessing as mp
+    from conftest import case_dir
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / ("dist_%s.vaf" % entry["name"]))
+    res = str(tmp_path / "res.json")
+    mp.start_processes(_driver_rank, args=(world, port, entry["argv"] + ["-o", out], case_dir(entry, synth_dir), res,
+                                           counter), nprocs=world, join=True, start_method="spawn")
+    ranks = [json.load(open(res + ".%d" % r)) for r in range(world)]
+    stats = {}
+    for key, pat in (("bases", "Bases processed:"), ("seqs", "Sequences processed:"), ("kmers", "K-mers extracted:")):
+        for line in ranks[0]["stderr"].splitlines():
+            if pat in line:
+                stats[key] = int(line.split(":")[1].split()[0])
+    data = open(out, "rb").read() if os.path.exists(out) else None
+    return [r["rc"] for r in ranks], stats, data, ranks[0]["stderr"]
+
+
+@pytest.mark.parametrize("counter", ["oracle", pytest.param("hip", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("name", DIST_CASES)
+def test_dist_driver_matches_reference(name, counter, manifest, synth_dir, tmp_path):
+    """vafc_dist.run over two gloo ranks (the oracle as the per-rank counter on
+    CPU; the HIP counter, both ranks on device 0, in the GPU suite): the files
+    are dealt over the ranks, the counts all-reduced, and rank 0's .vaf and -v
+    tallies equal the reference's."""
+    import hashlib
+    entry = next(c for c in manifest["cases"] if c["name"] == name)
+    rcs, stats, data, err = _run_driver(entry, synth_dir, tmp_path, counter)
+    assert rcs == [entry["exit"]] * 2, err[-2000:]
+    assert hashlib.md5(data).hexdigest() == entry["vaf_md5"]
+    for key in ("bases", "seqs", "kmers"):
+        assert stats.get(key) == entry["stats"].get(key), key
+    assert ("collisions detected" in err) == entry["collision_warning"]
+
+
+def test_dist_driver_usage_and_missing_patterns(tmp_path):
+    """Usage errors and an unreadable pattern file exit 1 on every rank before
+    any collective (single-rank path of the same driver)."""
+    import vafc_dist as D
+    lines = []
+    assert D.run(["-p", "p.txt"], None, err=lines.append) == 1 and "Usage" in "".join(lines)
+    lines = []
+    assert D.run(["-p", str(tmp_path / "none.txt"), "-o", str(tmp_path / "o.vaf"), "x.fq"], None,
+                 err=lines.append) == 1
+    assert "failed to load pattern file" in "".join(lines)
