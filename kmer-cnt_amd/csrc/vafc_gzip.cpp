@@ -4,6 +4,7 @@
 // zlib (the reference's gzread, pinned by the system package) remains the
 // decoder of record for every chunk whose speculative decode is not used.
 #include "vafc_gzip.h"
+#include "vafc_affinity.h"
 
 #include <fcntl.h>
 #include <stdio.h>
@@ -1418,8 +1419,16 @@ bool VcGzParallel::start(const char *path, int threads, uint64_t chunk_bytes)
 	for (auto &s : slots_) s.reset(new Chunk);
 	max_pieces_ = (size_t)threads + extra + 2;
 	fixed_tables();
-	for (int t = 0; t < threads; ++t) workers_.emplace_back(&VcGzParallel::worker, this);
-	seq_ = std::thread(&VcGzParallel::sequencer, this);
+	const VcCpuSet cpus = vc_affinity_get();   // vc_count_file's placement (vafc_affinity.h)
+	for (int t = 0; t < threads; ++t)
+		workers_.emplace_back([this, cpus] {
+			vc_affinity_bind(cpus);
+			worker();
+		});
+	seq_ = std::thread([this, cpus] {
+		vc_affinity_bind(cpus);
+		sequencer();
+	});
 	return true;
 }
 

@@ -13,7 +13,9 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <ctype.h>
 #include <dlfcn.h>
+#include <sched.h>
 #include <fcntl.h>
 #include <limits.h>
 #include <math.h>
@@ -28,6 +30,7 @@
 #include <vector>
 
 #include "vafc.h"
+#include "vafc_affinity.h"
 #include "vafc_common.h"
 #include "vafc_fastq.h"
 #include "vafc_gzip.h"
@@ -272,6 +275,8 @@ struct vc_ctx {
 	// stream (ev_in), and the launch -> st (ev_out), so that vc_reset, vc_finish
 	// and the shard sum, all on st, stay ordered with it (created on first use)
 	hipEvent_t ev_in = nullptr, ev_out = nullptr;
+	VcCpuSet cpus;                    // the GPUs' NUMA-node CPUs for the reader threads (gpu_cpus)
+	int cpus_threads = -1;            // the thread count cpus was computed for
 	struct Kc *kc = nullptr;               // histogram mode (vc_kc_create)
 	// multi-GPU (vc_create_multi): this ctx is shard 0; rep[i - 1] is shard i
 	std::vector<vc_ctx *> rep;
@@ -1308,6 +1313,64 @@ static int sync_shards(vc_ctx *c)
 	return hipSetDevice(c->dev) == hipSuccess ? VC_OK : VC_EHIP;
 }
 
+// CPUs of the NUMA node(s) the counter's GPUs hang off (sysfs, from each
+// device's PCI bus id), within this process's affinity mask (vafc_affinity.h).
+// Off when VAFC_NUMA=0, when sysfs says nothing, or when the node offers fewer
+// CPUs of the mask than the reader has threads (or than the whole mask).
+static VcCpuSet gpu_cpus(vc_ctx *c, int threads)
+{
+	if (c->cpus_threads == threads) return c->cpus;
+	VcCpuSet out;
+	const char *ne = getenv("VAFC_NUMA");
+	cpu_set_t mask;
+	CPU_ZERO(&out.set);
+	if (!(ne && !strcmp(ne, "0")) && sched_getaffinity(0, sizeof mask, &mask) == 0) {
+		bool any_node = false, bad = false;
+		for (int i = 0; i < n_shards(c) && !bad; ++i) {
+			char bus[64] = {0}, path[256], buf[4096];
+			if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, shard_at(c, i)->dev) != hipSuccess) {
+				(void)hipGetLastError();
+				bad = true;
+				break;
+			}
+			for (char *q = bus; *q; ++q) *q = (char)tolower((unsigned char)*q);
+			snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+			FILE *f = fopen(path, "r");
+			int node = -1;
+			if (!f || fscanf(f, "%d", &node) != 1) node = -1;
+			if (f) fclose(f);
+			if (node < 0) {
+				bad = true;
+				break;
+			}
+			snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+			f = fopen(path, "r");
+			size_t n = f ? fread(buf, 1, sizeof buf - 1, f) : 0;
+			if (f) fclose(f);
+			buf[n] = 0;
+			for (char *q = buf; *q;) {   // "0-63,128-191"
+				char *e;
+				const long a = strtol(q, &e, 10);
+				if (e == q) break;
+				long b = a;
+				if (*e == '-') b = strtol(e + 1, &e, 10);
+				for (long x = a; x <= b && x < CPU_SETSIZE; ++x) CPU_SET((int)x, &out.set);
+				any_node = true;
+				q = *e == ',' ? e + 1 : e;
+				if (*e != ',') break;
+			}
+		}
+		if (!bad && any_node) {
+			CPU_AND(&out.set, &out.set, &mask);
+			const int have = CPU_COUNT(&out.set);
+			out.on = have >= threads && have < CPU_COUNT(&mask);
+		}
+	}
+	c->cpus = out;
+	c->cpus_threads = threads;
+	return out;
+}
+
 extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n_threads,
                              vc_file_stats *st)
 {
@@ -1315,6 +1378,8 @@ extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n
 	vc_file_stats local = {0, 0, 0, 0.0};
 	const double t0 = wall_now();
 	HIPCK(hipSetDevice(c->dev));
+	// the reader threads spawned below run on the GPU's NUMA node
+	VcAffinityScope placement(gpu_cpus(c, clamp_threads(n_threads)));
 	{
 		const int fd = open(path, O_RDONLY);
 		if (fd < 0) return VC_EIO;

@@ -1,5 +1,6 @@
 // vafc_ingest.cpp -- see vafc_ingest.h.
 #include "vafc_ingest.h"
+#include "vafc_affinity.h"
 
 #include <errno.h>
 #include <stdio.h>
@@ -65,7 +66,13 @@ private:
 // more (a record longer than the window must still be read).
 class GzSource : public VcIngestSource {
 public:
-	GzSource(VcGzParallel *g, uint64_t window) : g_(g), window_(window) { pump_ = std::thread([this] { pump(); }); }
+	GzSource(VcGzParallel *g, uint64_t window) : g_(g), window_(window)
+	{
+		pump_ = std::thread([this, cpus = vc_affinity_get()] {
+			vc_affinity_bind(cpus);
+			pump();
+		});
+	}
 	~GzSource() override
 	{
 		abort();
@@ -380,7 +387,9 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 	bool abort = false;
 	std::atomic<uint64_t> next{0};
 
+	const VcCpuSet cpus = vc_affinity_get();   // vc_count_file's placement (vafc_affinity.h)
 	auto worker = [&]() {
+		vc_affinity_bind(cpus);
 		VcFastqReader rd;
 		std::vector<uint8_t> tmp;
 		for (;;) {
