@@ -107,6 +107,17 @@ def cli_run(binary, pat, fq, threads, out, k, env=None, timeout=900):
             "bases": int(bases.group(1)) if bases else None}
 
 
+def cgroup_cpu_max():
+    """The process's cgroup v2 CPU quota ("max 100000" = none), or None."""
+    try:
+        with open("/proc/self/cgroup") as f:
+            rel = f.read().strip().split("::")[-1]
+        with open(os.path.join("/sys/fs/cgroup" + rel, "cpu.max")) as f:
+            return f.read().strip()
+    except (OSError, IndexError):
+        return None
+
+
 def md5(path):
     h = hashlib.md5()
     with open(path, "rb") as f:
@@ -243,6 +254,7 @@ def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None, dev=None, device_
                            n_reads // 1_000_000, L, n_reads * L / 1e9, fq_bytes / 1e9,
                            "tmpfs" if work.startswith("/dev/shm") else "disk", k),
            "reads": n_reads, "threads": t, "host_cpus": os.cpu_count(), "cpu_share": cpu_share(),
+           "cgroup_cpu_max": cgroup_cpu_max(),
            "timer": "CLI -v Speed line: bases / counting-phase wall clock (from the first file open, the "
                     "reader's buffer allocation included, to the counts on the host), as the reference's "
                     "vaf-counter.c:646-651,707; process start, HIP init and table upload are outside it, "
@@ -257,9 +269,14 @@ def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None, dev=None, device_
                             "one shard per GPU, one RCCL reduce of the counts before the .vaf is written"
                             % len(devices))
     vafs = {}
+    n_runs = int(os.environ.get("VAFC_E2E_RUNS", "5"))
     for name, path in (("plain", fq), ("gzip", gz)):
+        # one untimed run first: the first pass over a freshly written 31.5 GB
+        # file ran at half speed or less on every box (profiles/r04c_n8_projection.json,
+        # profiles/r04c_numa_ab.json: 7.4 and 14.0 Gbases/s against 15-27 after it)
+        cli_run(PRODUCT_CLI, pat, path, t, os.path.join(tmp, "e2e_warm.vaf"), k, env=env, timeout=180)
         runs = []
-        for rep in range(3):
+        for rep in range(n_runs):
             o = os.path.join(tmp, "e2e_%s.vaf" % name)
             # a run takes seconds; a hang (e.g. in a multi-GPU RCCL set-up) ends the
             # leg after 3 minutes instead of holding the whole bench line back
@@ -277,7 +294,8 @@ def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None, dev=None, device_
                      "process_wall_s": round(med["wall"], 3),
                      "process_mbases": round(med["bases"] / med["wall"] / 1e6, 1) if med["bases"] else None,
                      "kmers_per_sec": med["mkmers"] * 1e6 if med["mkmers"] else None,
-                     "runs": [r["mbases"] for r in runs]}
+                     "runs": [r["mbases"] for r in runs],
+                     "runs_note": "after one untimed run; value = median"}
     bases = n_reads * L
     out["gzip"]["format"] = ("one gzip member, zlib level 1 (gzip -1's algorithm), compressed the way pigz "
                              "does (16 MB pieces, 32 KiB dictionary carried, sync-flushed), %.2f GB" % (gz_bytes / 1e9))
