@@ -290,6 +290,8 @@ def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None, dev=None, device_
         out[name] = {"value": med["mbases"], "unit": "Mbases/sec",
                      "min": srt[0]["mbases"], "median": med["mbases"], "max": srt[-1]["mbases"],
                      "spread": round((srt[-1]["mbases"] - srt[0]["mbases"]) / med["mbases"], 3),
+                     "spread_inner": round((srt[-2]["mbases"] - srt[1]["mbases"]) / med["mbases"], 3)
+                     if len(srt) >= 4 else None,
                      "counting_s": round(med["bases"] / (med["mbases"] * 1e6), 3) if med["bases"] else None,
                      "process_wall_s": round(med["wall"], 3),
                      "process_mbases": round(med["bases"] / med["wall"] / 1e6, 1) if med["bases"] else None,
