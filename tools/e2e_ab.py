@@ -27,7 +27,9 @@ def main():
     ap.add_argument("--reads", type=int, default=100_000_000)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--gzip", action="store_true")
+    ap.add_argument("--gzip", action="store_true", help="pigz-shaped gzip level 1 (bench.py's e2e file)")
+    ap.add_argument("--gzip-single", action="store_true",
+                    help="one plain zlib level-1 deflate stream (gzip -1's shape: no sync-flushed pieces)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import numpy as np
@@ -59,6 +61,13 @@ def main():
         path = fq + ".gz"
         bench.gzip_level1(fq, path, a.threads)
         os.unlink(fq)
+    elif a.gzip_single:
+        import gzip
+        path = fq + ".gz"
+        with open(fq, "rb") as f, gzip.GzipFile(path, "wb", compresslevel=1, mtime=0) as g:
+            for b in iter(lambda: f.read(16 << 20), b""):
+                g.write(b)
+        os.unlink(fq)
     specs = []
     for v in a.variants:
         name, rest = v.split("=", 1)
@@ -69,7 +78,8 @@ def main():
             env[k_] = val
         specs.append((name, os.path.join(ROOT, parts[0]), env))
     out = {"workload": "%dM x %d bp reads of the C2 stream, %s, -t %d" % (
-        R // 1_000_000, L, "gzip level 1" if a.gzip else "plain FASTQ", a.threads), "runs": {}}
+        R // 1_000_000, L, "gzip level 1, pigz-shaped" if a.gzip else
+        ("gzip level 1, one stream (gzip -1 shape)" if a.gzip_single else "plain FASTQ"), a.threads), "runs": {}}
     md5s = {}
     for name, cli, env in specs:   # one untimed pass each: the first pass over a fresh file is slow
         bench.cli_run(cli, pat, path, a.threads, os.path.join(tmp, "warm.vaf"), 21, env=env, timeout=300)
