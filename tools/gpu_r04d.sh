@@ -6,5 +6,5 @@ bash tools/r03_ab.sh $O/r04d_ab_hb.log "default hb" --rounds 10 || { echo AB_FAI
 grep -E "^==|median|identical" $O/r04d_ab_hb.log
 bash tools/r03_ab.sh $O/r04d_ab_c5.log "default ba2 hb" --rounds 6 --panel syn200k || { echo AB5_FAILED; tail -20 $O/r04d_ab_c5.log; exit 1; }
 grep -E "^==|median|identical" $O/r04d_ab_c5.log
-timeout -k 10 900 python tools/e2e_ab.py --rounds 6 numa=kmer-cnt_amd/lib_ab/numa/vaf-counter nonuma=kmer-cnt_amd/lib_ab/numa/vaf-counter,VAFC_NUMA=0 > $O/r04d_numa_ab.json 2> $O/r04d_numa_ab.err || { echo NUMA_AB_FAILED; tail -20 $O/r04d_numa_ab.err; exit 1; }
+timeout -k 10 900 python tools/e2e_ab.py --rounds 6 numa=kmer-cnt_amd/lib/vaf-counter nonuma=kmer-cnt_amd/lib/vaf-counter,VAFC_NUMA=0 > $O/r04d_numa_ab.json 2> $O/r04d_numa_ab.err || { echo NUMA_AB_FAILED; tail -20 $O/r04d_numa_ab.err; exit 1; }
 cat $O/r04d_numa_ab.json
