@@ -8,7 +8,8 @@ line and each variant's min / median / max / spread.
     python tools/e2e_ab.py [--reads N] [--gzip] [--threads 16] [--rounds 5] \\
         numa=kmer-cnt_amd/lib_ab/numa/vaf-counter nonuma=kmer-cnt_amd/lib_ab/numa/vaf-counter,VAFC_NUMA=0
 
-A variant is NAME=CLI[,KEY=VAL...] (CLI relative to the repository root).
+A variant is NAME=CLI[,KEY=VAL...] (CLI relative to the repository root);
+the key T sets that variant's -t instead of --threads.
 """
 import argparse
 import json
@@ -20,6 +21,15 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "kmer-cnt_amd"))
+
+
+def cpu_stat():
+    """cgroup v2 cpu.stat (throttling counters), {} if unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (l.split() for l in f if l.strip())}
+    except (OSError, ValueError):
+        return {}
 
 
 def main():
@@ -73,21 +83,32 @@ def main():
         name, rest = v.split("=", 1)
         parts = rest.split(",")
         env = dict(os.environ)
+        thr = a.threads
         for kv in parts[1:]:
             k_, val = kv.split("=", 1)
-            env[k_] = val
-        specs.append((name, os.path.join(ROOT, parts[0]), env))
+            if k_ == "T":
+                thr = int(val)
+            else:
+                env[k_] = val
+        specs.append((name, os.path.join(ROOT, parts[0]), env, thr))
     out = {"workload": "%dM x %d bp reads of the C2 stream, %s, -t %d" % (
         R // 1_000_000, L, "gzip level 1, pigz-shaped" if a.gzip else
         ("gzip level 1, one stream (gzip -1 shape)" if a.gzip_single else "plain FASTQ"), a.threads), "runs": {}}
     md5s = {}
-    for name, cli, env in specs:   # one untimed pass each: the first pass over a fresh file is slow
-        bench.cli_run(cli, pat, path, a.threads, os.path.join(tmp, "warm.vaf"), 21, env=env, timeout=300)
+    for name, cli, env, thr in specs:   # one untimed pass each: the first pass over a fresh file is slow
+        bench.cli_run(cli, pat, path, thr, os.path.join(tmp, "warm.vaf"), 21, env=env, timeout=300)
     for rep in range(a.rounds):
-        for name, cli, env in specs:
+        for name, cli, env, thr in specs:
             o = os.path.join(tmp, name + ".vaf")
-            r = bench.cli_run(cli, pat, path, a.threads, o, 21, env=env, timeout=300)
+            c0 = cpu_stat()
+            r = bench.cli_run(cli, pat, path, thr, o, 21, env=env, timeout=300)
+            c1 = cpu_stat()
             out["runs"].setdefault(name, []).append(r["mbases"])
+            if c0 and c1:
+                out.setdefault("throttled_ms", {}).setdefault(name, []).append(
+                    round((c1.get("throttled_usec", 0) - c0.get("throttled_usec", 0)) / 1000, 1))
+                out.setdefault("cpu_s", {}).setdefault(name, []).append(
+                    round((c1.get("usage_usec", 0) - c0.get("usage_usec", 0)) / 1e6, 2))
             md5s[name] = bench.md5(o)
             sys.stderr.write("[e2e_ab] %s round %d: %.1f Mbases/s\n" % (name, rep + 1, r["mbases"]))
     for name, xs in out["runs"].items():
