@@ -103,8 +103,9 @@ def cli_run(binary, pat, fq, threads, out, k, env=None, timeout=900):
     bases = re.search(r"Bases processed:\s+([0-9]+)", p.stderr)
     if p.returncode != 0 or not m:
         raise RuntimeError("%s failed: %s" % (binary, p.stderr[-2000:]))
+    diag = re.findall(r"^\[(?:ingest|P::main)\].*$", p.stderr, re.M)   # VAFC_INGEST_PROFILE / VAFC_PHASES lines
     return {"mbases": float(m.group(1)), "mkmers": float(km.group(1)) if km else None, "wall": wall,
-            "bases": int(bases.group(1)) if bases else None}
+            "bases": int(bases.group(1)) if bases else None, "diag": diag}
 
 
 def cgroup_cpu_max():

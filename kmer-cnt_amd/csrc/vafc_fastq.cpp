@@ -53,8 +53,27 @@ bool VcFastqReader::open_src(VcTextSource *src, uint64_t off, size_t window)
 	return buf_ != nullptr;
 }
 
+bool VcFastqReader::open_view(const uint8_t *p, uint64_t n, uint64_t off)
+{
+	close();
+	view_ = true;
+	buf_ = (uint8_t *)p;
+	cap_ = (size_t)n;
+	base_ = foff_ = off;
+	b_ = 0;
+	e_ = (size_t)n;
+	eof_ = false;
+	hdr_ = 0;
+	return p != nullptr || n == 0;
+}
+
 void VcFastqReader::close()
 {
+	if (view_) {
+		buf_ = nullptr;   // not owned
+		view_ = false;
+	}
+	seqp_ = nullptr;
 	if (fp_) gzclose(fp_);
 	fp_ = nullptr;
 	if (gzp_) {
@@ -70,6 +89,11 @@ void VcFastqReader::close()
 bool VcFastqReader::refill()
 {
 	if (eof_) return false;
+	if (view_) {   // the whole text is in the window already
+		eof_ = true;
+		b_ = e_;
+		return false;
+	}
 	ssize_t n;
 	if (src_) {
 		n = (ssize_t)src_->read(buf_, cap_, foff_);
@@ -202,23 +226,44 @@ int VcFastqReader::next()
 	int c, d;
 	if (!hdr_ && peek_header() < 0) return -1;   // scan to a '>' or '@' (kseq.h:197-201)
 	seq_.l = name_.l = 0;
+	seqp_ = nullptr;
 	if (token(&d) < 0) return -1;
 	if (d != '\n' && !at_end()) skip_line();          // comment (kseq.h:204)
-	// sequence lines until a line starts with '+', '>' or '@' (kseq.h:209-213)
-	while ((c = getc_()) != -1 && c != '>' && c != '+' && c != '@') {
-		if (c == '\n') continue;
-		seq_.push(c);
-		line(&seq_);
+	c = -1;
+	if (view_ && b_ < e_) {
+		// In place: a sequence of one line followed by a line starting with
+		// '+', '>' or '@' is exactly what the loop below would collect (its
+		// first byte, then line()'s rest of the line with the CR rule), so it
+		// is handed out as a pointer instead of being copied.
+		const uint8_t *p = buf_ + b_;
+		const uint8_t *nl = (const uint8_t *)memchr(p, '\n', e_ - b_);
+		if (nl && nl + 1 < buf_ + e_ && *p != '\n' && *p != '>' && *p != '+' && *p != '@' &&
+		    (nl[1] == '+' || nl[1] == '>' || nl[1] == '@')) {
+			size_t l = (size_t)(nl - p);
+			if (l > 1 && p[l - 1] == '\r') --l;
+			seqp_ = (const char *)p;
+			seql_ = l;
+			b_ = (size_t)(nl - buf_) + 2;
+			c = nl[1];
+		}
 	}
+	// sequence lines until a line starts with '+', '>' or '@' (kseq.h:209-213)
+	if (!seqp_)
+		while ((c = getc_()) != -1 && c != '>' && c != '+' && c != '@') {
+			if (c == '\n') continue;
+			seq_.push(c);
+			line(&seq_);
+		}
 	if (c == '>' || c == '@') {
 		hdr_ = c;
 		hdr_pos_ = last_pos();
 	}
-	if (c != '+') return (int)seq_.l;                 // FASTA
+	const size_t sl = seq_len();
+	if (c != '+') return (int)sl;                     // FASTA
 	do c = getc_(); while (c != -1 && c != '\n');     // rest of the '+' line
 	if (c == -1) return -2;
 	size_t ql = 0, qcr = 0;
-	while (qual_line(&ql, &qcr) >= 0 && ql < seq_.l) {}
+	while (qual_line(&ql, &qcr) >= 0 && ql < sl) {}
 	hdr_ = 0;
-	return seq_.l == ql ? (int)seq_.l : -2;
+	return sl == ql ? (int)sl : -2;
 }

@@ -26,6 +26,15 @@ public:
 	// Up to n bytes at offset off into p, waiting until they exist; fewer
 	// than n only at the end of the text (or after the source was aborted).
 	virtual int64_t read(uint8_t *p, size_t n, uint64_t off) = 0;
+	// The whole text from offset off on, in place (a memory-mapped file):
+	// a pointer to byte off and, in *avail, the bytes from there to the end
+	// of the text; nullptr if the source has no such view (read() then).
+	virtual const uint8_t *view(uint64_t off, uint64_t *avail)
+	{
+		(void)off;
+		*avail = 0;
+		return nullptr;
+	}
 };
 
 class VcByteBuf {
@@ -65,14 +74,19 @@ public:
 	// source (not owned).  `off` must be where kseq would look for a
 	// record's header.
 	bool open_src(VcTextSource *src, uint64_t off, size_t window = (size_t)4 << 20);
+	// As open_src, over text held in place (VcTextSource::view): p is the
+	// byte at text offset `off`, n the bytes from there to the end of the
+	// text.  Nothing is copied in; a one-line sequence is handed out as a
+	// pointer into the text (seq()).
+	bool open_view(const uint8_t *p, uint64_t n, uint64_t off);
 	void close();
 	int next();
 	// File offset of the next record's header character ('@' or '>'),
 	// scanning forward like next() does; -1 at end of input.  next() then
 	// parses that record.
 	int64_t peek_header();
-	const char *seq() const { return seq_.s; }
-	size_t seq_len() const { return seq_.l; }
+	const char *seq() const { return seqp_ ? seqp_ : seq_.s; }
+	size_t seq_len() const { return seqp_ ? seql_ : seq_.l; }
 	// keep record names (kseq's name: the header up to the first isspace byte)
 	void keep_names(bool on) { keep_name_ = on; }
 	const char *name() const { return name_.s ? name_.s : ""; }
@@ -86,6 +100,9 @@ private:
 	uint64_t base_ = 0;           // text offset of buf_[0] (source reads)
 	uint8_t *buf_ = nullptr;
 	size_t cap_ = 0, b_ = 0, e_ = 0;
+	bool view_ = false;           // buf_ is the caller's text (open_view), not owned
+	const char *seqp_ = nullptr;  // this record's sequence in place (view only), else seq_
+	size_t seql_ = 0;
 	bool eof_ = false;
 	int hdr_ = 0;                 // header char already consumed, 0 if none
 	uint64_t hdr_pos_ = 0;        // its text offset (source reads)

@@ -7,6 +7,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -46,16 +47,44 @@ ssize_t pread_full(int fd, uint8_t *p, size_t n, uint64_t off)
 	return (ssize_t)got;
 }
 
-// A plain file through pread.
+// A plain file, mapped read-only: the parse workers read the page cache in
+// place (VcTextSource::view) instead of pread-copying every byte into their
+// windows first -- on the whole C2 stream that copy was a third of the
+// pass's memory traffic, and the plain pass is memory-bound (DESIGN.md
+// section 7).  pread when the file cannot be mapped, or with VAFC_MMAP=0.
 class FdSource : public VcIngestSource {
 public:
-	FdSource(int fd, uint64_t size) : fd_(fd), size_(size) {}
-	int64_t read(uint8_t *p, size_t n, uint64_t off) override { return pread_full(fd_, p, n, off); }
+	FdSource(int fd, uint64_t size) : fd_(fd), size_(size)
+	{
+		const char *e = getenv("VAFC_MMAP");
+		if (size_ > 0 && !(e && e[0] == '0')) {
+			void *m = mmap(nullptr, (size_t)size_, PROT_READ, MAP_SHARED, fd_, 0);
+			if (m != MAP_FAILED) map_ = (const uint8_t *)m;
+		}
+	}
+	~FdSource() override
+	{
+		if (map_) munmap((void *)map_, (size_t)size_);
+	}
+	int64_t read(uint8_t *p, size_t n, uint64_t off) override
+	{
+		if (!map_) return pread_full(fd_, p, n, off);
+		if (off >= size_) return 0;
+		const size_t got = size_ - off < n ? (size_t)(size_ - off) : n;
+		memcpy(p, map_ + off, got);
+		return (int64_t)got;
+	}
+	const uint8_t *view(uint64_t off, uint64_t *avail) override
+	{
+		*avail = map_ && off < size_ ? size_ - off : 0;
+		return map_ && off <= size_ ? map_ + off : nullptr;
+	}
 	bool longer_than(uint64_t off) override { return size_ > off; }
 
 private:
 	int fd_;
 	uint64_t size_;
+	const uint8_t *map_ = nullptr;
 };
 
 // A gzip file's text: a pump thread takes the inflater's output in order as
@@ -221,10 +250,18 @@ int64_t guess_record(VcTextSource &src, uint64_t a, bool fasta, std::vector<uint
 {
 	const uint64_t from = a - 1;
 	const size_t want = (size_t)1 << 20;
-	tmp.resize(want);
-	const int64_t got = src.read(tmp.data(), want, from);
+	uint64_t avail = 0;
+	const uint8_t *s = src.view(from, &avail);
+	int64_t got;
+	if (s) {
+		got = (int64_t)(avail < want ? avail : want);
+	} else {
+		tmp.resize(want);
+		got = src.read(tmp.data(), want, from);
+		s = tmp.data();
+	}
 	if (got < 2) return -1;
-	const uint8_t *s = tmp.data(), *e = s + got;
+	const uint8_t *e = s + got;
 	const bool at_eof = (size_t)got < want;   // a short read ends at the end of the text
 	for (const uint8_t *p = s + 1; p < e; ++p) {
 		if (p[-1] != '\n') {
@@ -264,7 +301,9 @@ int parse_piece(VcTextSource &src, uint64_t start, int k, int slot, VcIngestSink
 	P.errs.clear();
 	P.eof = false;
 	P.end = start;
-	if (!rd.open_src(&src, start, (size_t)1 << 20)) return VC_ENOMEM;
+	uint64_t avail = 0;
+	const uint8_t *v = src.view(start, &avail);
+	if (!(v ? rd.open_view(v, avail, start) : rd.open_src(&src, start, (size_t)1 << 20))) return VC_ENOMEM;
 	size_t used = 0;
 	for (;;) {
 		const int64_t h = rd.peek_header();

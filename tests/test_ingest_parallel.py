@@ -43,6 +43,21 @@ def test_fuzzed_inputs(seed, tmp_path):
             _same(p, k, b, threads=1 + seed % 5, piece=piece)
 
 
+@pytest.mark.parametrize("mmap", ["0", "1"])
+@pytest.mark.parametrize("seed", range(4))
+def test_fuzzed_inputs_pread_and_mapped(seed, mmap, tmp_path, monkeypatch):
+    """Both plain-file sources of the parallel reader: pread into each
+    worker's window (VAFC_MMAP=0) and the mapped file parsed in place, where
+    one-line sequences are handed out as pointers into the text."""
+    monkeypatch.setenv("VAFC_MMAP", mmap)
+    rng = np.random.default_rng(900 + seed)
+    p = str(tmp_path / "fuzz.fq")
+    _fuzz_file(p, rng, 300)
+    for piece in (5, 97, 4096):
+        for k, b in ((5, 10_000_000), (3, 1), (12, 50)):
+            _same(p, k, b, threads=2 + seed % 3, piece=piece)
+
+
 def _fastq(path, rng, n, L=150, crlf=False):
     nl = b"\r\n" if crlf else b"\n"
     with open(path, "wb") as f:

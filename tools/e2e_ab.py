@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--gzip", action="store_true", help="pigz-shaped gzip level 1 (bench.py's e2e file)")
     ap.add_argument("--gzip-single", action="store_true",
                     help="one plain zlib level-1 deflate stream (gzip -1's shape: no sync-flushed pieces)")
+    ap.add_argument("--host-parse", action="store_true",
+                    help="also time the parallel reader alone (vc_scan_file_parallel, no GPU) under each variant's env")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import numpy as np
@@ -104,6 +106,8 @@ def main():
             r = bench.cli_run(cli, pat, path, thr, o, 21, env=env, timeout=300)
             c1 = cpu_stat()
             out["runs"].setdefault(name, []).append(r["mbases"])
+            if r.get("diag"):
+                out.setdefault("diag", {}).setdefault(name, []).append(r["diag"])
             if c0 and c1:
                 out.setdefault("throttled_ms", {}).setdefault(name, []).append(
                     round((c1.get("throttled_usec", 0) - c0.get("throttled_usec", 0)) / 1000, 1))
@@ -111,6 +115,23 @@ def main():
                     round((c1.get("usage_usec", 0) - c0.get("usage_usec", 0)) / 1e6, 2))
             md5s[name] = bench.md5(o)
             sys.stderr.write("[e2e_ab] %s round %d: %.1f Mbases/s\n" % (name, rep + 1, r["mbases"]))
+    if a.host_parse:   # the reader alone: pieces parsed into host slots, nothing shipped
+        import time
+        for rep in range(a.rounds):
+            for name, cli, env, thr in specs:
+                saved = {k_: os.environ.get(k_) for k_ in env if k_.startswith("VAFC_")}
+                for k_ in saved:
+                    os.environ[k_] = env[k_]
+                t = time.time()
+                vafc.scan_file_parallel(path, 21, 10_000_000, threads=thr, piece_bytes=16 << 20)
+                dt = time.time() - t
+                for k_, v_ in saved.items():
+                    if v_ is None:
+                        os.environ.pop(k_, None)
+                    else:
+                        os.environ[k_] = v_
+                out.setdefault("host_parse_gbs", {}).setdefault(name, []).append(
+                    round(os.path.getsize(path) / dt / 1e9, 2))
     for name, xs in out["runs"].items():
         s = sorted(xs)
         med = s[len(s) // 2]
