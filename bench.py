@@ -113,10 +113,17 @@ def cgroup_cpu_max():
     try:
         with open("/proc/self/cgroup") as f:
             rel = f.read().strip().split("::")[-1]
-        with open(os.path.join("/sys/fs/cgroup" + rel, "cpu.max")) as f:
-            return f.read().strip()
     except (OSError, IndexError):
-        return None
+        rel = ""
+    # the cgroup's own directory, or the namespace root (a container's cgroup
+    # namespace shows its cgroup as "/" while /proc/self/cgroup names the host path)
+    for d in ("/sys/fs/cgroup" + rel, "/sys/fs/cgroup"):
+        try:
+            with open(os.path.join(d, "cpu.max")) as f:
+                return f.read().strip()
+        except OSError:
+            continue
+    return None
 
 
 def md5(path):

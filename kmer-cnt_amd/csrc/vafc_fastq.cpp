@@ -94,6 +94,11 @@ bool VcFastqReader::refill()
 		b_ = e_;
 		return false;
 	}
+	if (seqp_) {   // the window is about to be replaced: keep this record's sequence
+		seq_.l = 0;
+		seq_.append((const uint8_t *)seqp_, seql_);
+		seqp_ = nullptr;
+	}
 	ssize_t n;
 	if (src_) {
 		n = (ssize_t)src_->read(buf_, cap_, foff_);
@@ -227,14 +232,51 @@ int VcFastqReader::next()
 	if (!hdr_ && peek_header() < 0) return -1;   // scan to a '>' or '@' (kseq.h:197-201)
 	seq_.l = name_.l = 0;
 	seqp_ = nullptr;
+	static const bool inplace = !(getenv("VAFC_SEQ_INPLACE") && getenv("VAFC_SEQ_INPLACE")[0] == '0');   // A/B knob
+	if (inplace && hdr_ == '@' && !keep_name_ && b_ < e_) {
+		// A whole four-line FASTQ record inside the window, located with four
+		// memchr and taken only if every step below would take the common
+		// branch: the header's rest up to its '\n' (the name token and the
+		// comment are discarded, kseq.h:203-204), one sequence line followed by
+		// a '+' line, and one quality line at least as long as the sequence
+		// (kseq.h:209-229, each line with line()'s CR rule).  Anything else --
+		// a record that crosses the window, wrapped sequences or qualities,
+		// names kept -- falls through to the byte-wise path below, nothing
+		// consumed.
+		const uint8_t *p = buf_ + b_, *e = buf_ + e_;
+		const uint8_t *n1 = (const uint8_t *)memchr(p, '\n', (size_t)(e - p));
+		const uint8_t *sq = n1 ? n1 + 1 : e;
+		if (sq < e && *sq != '\n' && *sq != '>' && *sq != '+' && *sq != '@') {
+			const uint8_t *n2 = (const uint8_t *)memchr(sq, '\n', (size_t)(e - sq));
+			if (n2 && n2 + 1 < e && n2[1] == '+') {
+				const uint8_t *n3 = (const uint8_t *)memchr(n2 + 1, '\n', (size_t)(e - n2 - 1));
+				const uint8_t *q = n3 ? n3 + 1 : e;
+				const uint8_t *n4 = q < e ? (const uint8_t *)memchr(q, '\n', (size_t)(e - q)) : nullptr;
+				if (n4) {
+					size_t sl = (size_t)(n2 - sq);
+					if (sl > 1 && sq[sl - 1] == '\r') --sl;
+					size_t ql = (size_t)(n4 - q);
+					if (ql > 1 && q[ql - 1] == '\r') --ql;
+					if (ql >= sl) {
+						seqp_ = (const char *)sq;
+						seql_ = sl;
+						b_ = (size_t)(n4 + 1 - buf_);
+						hdr_ = 0;
+						return sl == ql ? (int)sl : -2;
+					}
+				}
+			}
+		}
+	}
 	if (token(&d) < 0) return -1;
 	if (d != '\n' && !at_end()) skip_line();          // comment (kseq.h:204)
 	c = -1;
-	if (view_ && b_ < e_) {
+	if (inplace && b_ < e_) {
 		// In place: a sequence of one line followed by a line starting with
 		// '+', '>' or '@' is exactly what the loop below would collect (its
 		// first byte, then line()'s rest of the line with the CR rule), so it
-		// is handed out as a pointer instead of being copied.
+		// is handed out as a pointer into the window instead of being copied
+		// (refill() copies it out before the window is replaced).
 		const uint8_t *p = buf_ + b_;
 		const uint8_t *nl = (const uint8_t *)memchr(p, '\n', e_ - b_);
 		if (nl && nl + 1 < buf_ + e_ && *p != '\n' && *p != '>' && *p != '+' && *p != '@' &&

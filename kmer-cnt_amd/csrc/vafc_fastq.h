@@ -76,8 +76,7 @@ public:
 	bool open_src(VcTextSource *src, uint64_t off, size_t window = (size_t)4 << 20);
 	// As open_src, over text held in place (VcTextSource::view): p is the
 	// byte at text offset `off`, n the bytes from there to the end of the
-	// text.  Nothing is copied in; a one-line sequence is handed out as a
-	// pointer into the text (seq()).
+	// text.  Nothing is copied in.
 	bool open_view(const uint8_t *p, uint64_t n, uint64_t off);
 	void close();
 	int next();
@@ -85,6 +84,9 @@ public:
 	// scanning forward like next() does; -1 at end of input.  next() then
 	// parses that record.
 	int64_t peek_header();
+	// The record's sequence: a one-line sequence whose line ends inside the
+	// current window is a pointer into the window (valid until the next
+	// next() call), anything else the reader's own copy.
 	const char *seq() const { return seqp_ ? seqp_ : seq_.s; }
 	size_t seq_len() const { return seqp_ ? seql_ : seq_.l; }
 	// keep record names (kseq's name: the header up to the first isspace byte)
@@ -101,7 +103,7 @@ private:
 	uint8_t *buf_ = nullptr;
 	size_t cap_ = 0, b_ = 0, e_ = 0;
 	bool view_ = false;           // buf_ is the caller's text (open_view), not owned
-	const char *seqp_ = nullptr;  // this record's sequence in place (view only), else seq_
+	const char *seqp_ = nullptr;  // this record's sequence in the window, else seq_
 	size_t seql_ = 0;
 	bool eof_ = false;
 	int hdr_ = 0;                 // header char already consumed, 0 if none

@@ -47,17 +47,18 @@ ssize_t pread_full(int fd, uint8_t *p, size_t n, uint64_t off)
 	return (ssize_t)got;
 }
 
-// A plain file, mapped read-only: the parse workers read the page cache in
-// place (VcTextSource::view) instead of pread-copying every byte into their
-// windows first -- on the whole C2 stream that copy was a third of the
-// pass's memory traffic, and the plain pass is memory-bound (DESIGN.md
-// section 7).  pread when the file cannot be mapped, or with VAFC_MMAP=0.
+// A plain file through pread into each worker's window.  VAFC_MMAP=1 maps
+// the file instead and the workers parse the page cache in place
+// (VcTextSource::view): no copy, but on the box's tmpfs-cached C2 stream the
+// page faults of 16 threads cost more than the copies they save -- the
+// reader alone 34 against 57 GB/s of text, the CLI 12.7 against 20.5
+// Gbases/s (profiles/r04g_mmap_ab.json).
 class FdSource : public VcIngestSource {
 public:
 	FdSource(int fd, uint64_t size) : fd_(fd), size_(size)
 	{
 		const char *e = getenv("VAFC_MMAP");
-		if (size_ > 0 && !(e && e[0] == '0')) {
+		if (size_ > 0 && e && e[0] == '1') {
 			void *m = mmap(nullptr, (size_t)size_, PROT_READ, MAP_SHARED, fd_, 0);
 			if (m != MAP_FAILED) map_ = (const uint8_t *)m;
 		}
@@ -303,7 +304,9 @@ int parse_piece(VcTextSource &src, uint64_t start, int k, int slot, VcIngestSink
 	P.end = start;
 	uint64_t avail = 0;
 	const uint8_t *v = src.view(start, &avail);
-	if (!(v ? rd.open_view(v, avail, start) : rd.open_src(&src, start, (size_t)1 << 20))) return VC_ENOMEM;
+	const char *we = getenv("VAFC_READER_WINDOW");   // test knob: the workers' window in bytes
+	const size_t win = we && atoll(we) > 0 ? (size_t)atoll(we) : (size_t)1 << 20;
+	if (!(v ? rd.open_view(v, avail, start) : rd.open_src(&src, start, win))) return VC_ENOMEM;
 	size_t used = 0;
 	for (;;) {
 		const int64_t h = rd.peek_header();

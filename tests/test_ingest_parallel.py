@@ -47,8 +47,9 @@ def test_fuzzed_inputs(seed, tmp_path):
 @pytest.mark.parametrize("seed", range(4))
 def test_fuzzed_inputs_pread_and_mapped(seed, mmap, tmp_path, monkeypatch):
     """Both plain-file sources of the parallel reader: pread into each
-    worker's window (VAFC_MMAP=0) and the mapped file parsed in place, where
-    one-line sequences are handed out as pointers into the text."""
+    worker's window (the default) and the mapped file parsed in place
+    (VAFC_MMAP=1); one-line sequences are handed out as pointers into the
+    window either way, copied out only when the window is refilled."""
     monkeypatch.setenv("VAFC_MMAP", mmap)
     rng = np.random.default_rng(900 + seed)
     p = str(tmp_path / "fuzz.fq")
@@ -56,6 +57,20 @@ def test_fuzzed_inputs_pread_and_mapped(seed, mmap, tmp_path, monkeypatch):
     for piece in (5, 97, 4096):
         for k, b in ((5, 10_000_000), (3, 1), (12, 50)):
             _same(p, k, b, threads=2 + seed % 3, piece=piece)
+
+
+@pytest.mark.parametrize("window", [1, 5, 64, 333])
+def test_tiny_reader_windows(window, tmp_path, monkeypatch):
+    """Workers' windows far smaller than a record: every one-line sequence
+    handed out in place is copied out when its window is refilled mid-record
+    (VAFC_READER_WINDOW, a test knob)."""
+    monkeypatch.setenv("VAFC_READER_WINDOW", str(window))
+    rng = np.random.default_rng(77 + window)
+    p = str(tmp_path / "fuzz.fq")
+    _fuzz_file(p, rng, 200)
+    for piece in (13, 4096):
+        for k, b in ((5, 10_000_000), (3, 1)):
+            _same(p, k, b, threads=3, piece=piece)
 
 
 def _fastq(path, rng, n, L=150, crlf=False):
