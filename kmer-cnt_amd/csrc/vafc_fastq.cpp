@@ -42,11 +42,19 @@ bool VcFastqReader::open_parallel(const char *path, int threads, uint64_t chunk_
 
 bool VcFastqReader::open_src(VcTextSource *src, uint64_t off, size_t window)
 {
+	// a worker reopens its reader for every piece: keep an owned window of
+	// the same size (a fresh 1 MB malloc is an mmap, first-touch faults and
+	// an munmap whose TLB shootdown stops every thread of the process)
+	uint8_t *keep = nullptr;
+	if (buf_ && !view_ && !gzp_ && cap_ == window) {
+		keep = buf_;
+		buf_ = nullptr;
+	}
 	close();
 	src_ = src;
 	foff_ = base_ = off;
 	cap_ = window;
-	buf_ = (uint8_t *)malloc(cap_);
+	buf_ = keep ? keep : (uint8_t *)malloc(cap_);
 	b_ = e_ = 0;
 	eof_ = false;
 	hdr_ = 0;
