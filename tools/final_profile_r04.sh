@@ -15,7 +15,9 @@ cd /tmp && export TMPDIR=/tmp
 for C in c2 c5; do
   step 300 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof_$C -o p --output-format csv -- \
     python3 $R/bench.py --config $C --steps 10 --warmup 2 --no-parity --no-e2e --no-cpu > $O/${TAG}_prof_$C.json 2> $O/${TAG}_prof_$C.err
+  python3 $R/tools/trace_avg.py $O/${TAG}_prof_$C/p_kernel_trace.csv vc_count_reads_kernel 10 > $O/${TAG}_prof_${C}_timed.json || exit 1
 done
 cd $R
 step 900 python tools/pmc.py $O/${TAG}_pmc_c2 --steps 2 --warmup 1 --no-cpu --no-e2e --no-parity > $O/${TAG}_pmc_c2.log 2>&1
+step 900 python tools/pmc.py $O/${TAG}_pmc_c5 --config c5 --steps 2 --warmup 1 --no-cpu --no-e2e --no-parity > $O/${TAG}_pmc_c5.log 2>&1
 echo done

@@ -2,7 +2,7 @@
 set -o pipefail
 R=$(pwd); O=$R/gpurun_out
 cat /proc/self/cgroup > $O/r04d_cgroup.txt 2>&1; cat /sys/fs/cgroup/cpu.max >> $O/r04d_cgroup.txt 2>&1; nproc >> $O/r04d_cgroup.txt; python -c "import os; print(len(os.sched_getaffinity(0)))" >> $O/r04d_cgroup.txt
-bash tools/r03_ab.sh $O/r04d_ab_hb.log "default hb" --rounds 10 || { echo AB_FAILED; tail -20 $O/r04d_ab_hb.log; exit 1; }
+bash tools/r03_ab.sh $O/r04d_ab_hb.log "default hb fs" --rounds 10 || { echo AB_FAILED; tail -20 $O/r04d_ab_hb.log; exit 1; }
 grep -E "^==|median|identical" $O/r04d_ab_hb.log
 bash tools/r03_ab.sh $O/r04d_ab_c5.log "default ba2 hb" --rounds 6 --panel syn200k || { echo AB5_FAILED; tail -20 $O/r04d_ab_c5.log; exit 1; }
 grep -E "^==|median|identical" $O/r04d_ab_c5.log
