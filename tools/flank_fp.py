@@ -10,7 +10,7 @@ the four-test one of the kernels (distances VC_FLANK_DIST(k, 0..3)).  Each is
 queried with 4M uniform random k-mers and with the valid windows of 200k
 benchmark reads (C2's generator: 1 % of reads drawn over a SNP, so some
 passes are true hits; "true" = windows that are keys).
-    python tools/flank_fp.py
+    python tools/flank_fp.py [--extra]
 """
 import os
 import sys
@@ -89,5 +89,33 @@ def main():
                   % (K, tests, ds, len(keys), bm.mean(), 100 * passes(q), 100 * passes(win), 100 * true))
 
 
+def extra_tests():
+    """Round 4: more than four tests over the same bitmap (k = 21, on the
+    benchmark reads): every set is closed under d -> k - 10 - d, so the
+    bitmap stays closed under reverse complement."""
+    panel = S.make_panel(S.read_bed(S.default_bed_path()))
+    reads = S.gen_reads(panel, 200_000)
+    K = 21
+    d = tempfile.mkdtemp()
+    pat = os.path.join(d, "p.txt")
+    panel.write_patterns(pat, K)
+    keys, _, _ = vafc.load_patterns(pat).keys(K)
+    keys = np.unique(np.asarray(keys, dtype=np.uint64))
+    allk = np.concatenate([keys, revcomp(keys, K)])
+    win = read_windows(reads, K)
+    for ds in [(0, 4, 7, 11), (0, 3, 8, 11), (0, 2, 4, 7, 9, 11), (0, 2, 5, 6, 9, 11), (0, 1, 3, 8, 10, 11),
+               (0, 3, 5, 6, 8, 11)]:
+        bm = np.zeros(1 << 20, bool)
+        for dd in ds:
+            bm[(allk >> np.uint64(2 * dd)) & M] = True
+        ok = np.ones(win.size, bool)
+        for dd in ds:
+            ok &= bm[(win >> np.uint64(2 * dd)) & M]
+        print("k=21 distances=%s density %.3f reads %.4f%%" % (ds, bm.mean(), 100 * ok.mean()))
+
+
 if __name__ == "__main__":
-    main()
+    if "--extra" in sys.argv:
+        extra_tests()
+    else:
+        main()
