@@ -4,8 +4,71 @@
 
 #include <ctype.h>
 #include <stdlib.h>
+#include <string.h>
 #include <errno.h>
 #include <unistd.h>
+#include <immintrin.h>
+
+// The first up to four '\n' in [p, e), in order, into nl[]; returns how many.
+// One vector compare per 32 (16) bytes and a bit scan per line end, instead
+// of a memchr call per line (the record fast path of next() asks for four).
+__attribute__((target("avx2"))) static int newlines4_avx2(const uint8_t *p, const uint8_t *e, const uint8_t **nl)
+{
+	int n = 0;
+	const __m256i NL = _mm256_set1_epi8('\n');
+	for (; p + 32 <= e; p += 32) {
+		uint32_t m = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(_mm256_loadu_si256((const __m256i *)p), NL));
+		while (m) {
+			nl[n++] = p + __builtin_ctz(m);
+			if (n == 4) return 4;
+			m &= m - 1;
+		}
+	}
+	for (; p < e; ++p)
+		if (*p == '\n') {
+			nl[n++] = p;
+			if (n == 4) return 4;
+		}
+	return n;
+}
+
+static int newlines4_sse2(const uint8_t *p, const uint8_t *e, const uint8_t **nl)
+{
+	int n = 0;
+	const __m128i NL = _mm_set1_epi8('\n');
+	for (; p + 16 <= e; p += 16) {
+		uint32_t m = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i *)p), NL));
+		while (m) {
+			nl[n++] = p + __builtin_ctz(m);
+			if (n == 4) return 4;
+			m &= m - 1;
+		}
+	}
+	for (; p < e; ++p)
+		if (*p == '\n') {
+			nl[n++] = p;
+			if (n == 4) return 4;
+		}
+	return n;
+}
+
+static int newlines4_memchr(const uint8_t *p, const uint8_t *e, const uint8_t **nl)
+{
+	int n = 0;
+	while (n < 4 && p < e) {
+		const uint8_t *q = (const uint8_t *)memchr(p, '\n', (size_t)(e - p));
+		if (!q) break;
+		nl[n++] = q;
+		p = q + 1;
+	}
+	return n;
+}
+
+// VAFC_NL_SCAN=memchr: one memchr per line (the A/B baseline)
+static int (*const newlines4)(const uint8_t *, const uint8_t *, const uint8_t **) =
+	getenv("VAFC_NL_SCAN") && !strcmp(getenv("VAFC_NL_SCAN"), "memchr") ? newlines4_memchr
+	: __builtin_cpu_supports("avx2")                                     ? newlines4_avx2
+	                                                                     : newlines4_sse2;
 
 bool VcFastqReader::open(const char *path, size_t window)
 {
@@ -242,8 +305,8 @@ int VcFastqReader::next()
 	seqp_ = nullptr;
 	static const bool inplace = !(getenv("VAFC_SEQ_INPLACE") && getenv("VAFC_SEQ_INPLACE")[0] == '0');   // A/B knob
 	if (inplace && hdr_ == '@' && !keep_name_ && b_ < e_) {
-		// A whole four-line FASTQ record inside the window, located with four
-		// memchr and taken only if every step below would take the common
+		// A whole four-line FASTQ record inside the window, located by its
+		// first four line ends and taken only if every step below would take the common
 		// branch: the header's rest up to its '\n' (the name token and the
 		// comment are discarded, kseq.h:203-204), one sequence line followed by
 		// a '+' line, and one quality line at least as long as the sequence
@@ -252,26 +315,21 @@ int VcFastqReader::next()
 		// names kept -- falls through to the byte-wise path below, nothing
 		// consumed.
 		const uint8_t *p = buf_ + b_, *e = buf_ + e_;
-		const uint8_t *n1 = (const uint8_t *)memchr(p, '\n', (size_t)(e - p));
-		const uint8_t *sq = n1 ? n1 + 1 : e;
-		if (sq < e && *sq != '\n' && *sq != '>' && *sq != '+' && *sq != '@') {
-			const uint8_t *n2 = (const uint8_t *)memchr(sq, '\n', (size_t)(e - sq));
-			if (n2 && n2 + 1 < e && n2[1] == '+') {
-				const uint8_t *n3 = (const uint8_t *)memchr(n2 + 1, '\n', (size_t)(e - n2 - 1));
-				const uint8_t *q = n3 ? n3 + 1 : e;
-				const uint8_t *n4 = q < e ? (const uint8_t *)memchr(q, '\n', (size_t)(e - q)) : nullptr;
-				if (n4) {
-					size_t sl = (size_t)(n2 - sq);
-					if (sl > 1 && sq[sl - 1] == '\r') --sl;
-					size_t ql = (size_t)(n4 - q);
-					if (ql > 1 && q[ql - 1] == '\r') --ql;
-					if (ql >= sl) {
-						seqp_ = (const char *)sq;
-						seql_ = sl;
-						b_ = (size_t)(n4 + 1 - buf_);
-						hdr_ = 0;
-						return sl == ql ? (int)sl : -2;
-					}
+		const uint8_t *nl[4];
+		if (newlines4(p, e, nl) == 4) {
+			const uint8_t *n1 = nl[0], *n2 = nl[1], *n3 = nl[2], *n4 = nl[3];
+			const uint8_t *sq = n1 + 1, *q = n3 + 1;
+			if (*sq != '\n' && *sq != '>' && *sq != '+' && *sq != '@' && n2[1] == '+') {
+				size_t sl = (size_t)(n2 - sq);
+				if (sl > 1 && sq[sl - 1] == '\r') --sl;
+				size_t ql = (size_t)(n4 - q);
+				if (ql > 1 && q[ql - 1] == '\r') --ql;
+				if (ql >= sl) {
+					seqp_ = (const char *)sq;
+					seql_ = sl;
+					b_ = (size_t)(n4 + 1 - buf_);
+					hdr_ = 0;
+					return sl == ql ? (int)sl : -2;
 				}
 			}
 		}
