@@ -1242,7 +1242,9 @@ static int reserve_ingest_slots(vc_ctx *c, size_t slots);
 static int reserve_ingest(vc_ctx *c, int threads)
 {
 	const int N = n_shards(c);
-	const int slots = (threads + 2 + N - 1) / N * N;
+	const char *e = getenv("VAFC_INGEST_SLOTS");   // A/B knob: the reader's slot count (> threads)
+	const int want = e && atoi(e) > threads ? atoi(e) : threads + 2;
+	const int slots = (want + N - 1) / N * N;
 	for (int i = 0; i < N; ++i) {
 		vc_ctx *sh = shard_at(c, i);
 		HIPCK(hipSetDevice(sh->dev));
@@ -1264,7 +1266,9 @@ static int reserve_ingest_slots(vc_ctx *c, size_t slots)
 	for (size_t i = 0; i < slots; ++i) {
 		Slot &s = c->islot[i];
 		if (s.h_seq) continue;
-		int rc = slot_reserve(s, VC_PIECE_BYTES * 5 / 8 + ((size_t)1 << 20), VC_PIECE_BYTES / 256 + 4096);
+		// FASTQ: at most half of a piece's records' text is sequence (the
+		// quality line is as long); FASTA and long records grow the slot
+		int rc = slot_reserve(s, VC_PIECE_BYTES / 2 + ((size_t)256 << 10), VC_PIECE_BYTES / 256 + 4096);
 		if (rc != VC_OK) return rc;
 	}
 	return VC_OK;
