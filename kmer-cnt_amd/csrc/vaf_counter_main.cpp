@@ -120,8 +120,10 @@ int main(int argc, char *argv[])
 	fprintf(stderr, "[M::%s] Counting k-mers in FASTQ files with %d threads...\n", "main", n_thread);
 	t = now_s();
 	// the reader's pinned buffers are allocated inside the counting timer, as
-	// the reference allocates its per-block buffers inside it (vaf-counter.c:489-503)
-	rc = vc_reserve_file_ingest(ctx, n_thread);
+	// the reference allocates its per-block buffers inside it (vaf-counter.c:489-503):
+	// by vc_count_file's workers, each slot on its first use, overlapping the
+	// other workers' parsing (VAFC_RESERVE=1: all of them up front, as before)
+	rc = getenv("VAFC_RESERVE") && getenv("VAFC_RESERVE")[0] == '1' ? vc_reserve_file_ingest(ctx, n_thread) : VC_OK;
 	const double t_reserved = now_s();
 	if (rc != VC_OK) {
 		fprintf(stderr, "Error: counting failed (%s)\n", vc_strerror(rc));

@@ -1146,6 +1146,8 @@ double wall_now()
 #define VC_PIECE_BYTES ((uint64_t)16 << 20)
 #endif
 
+static int ingest_slot_alloc(Slot &s);
+
 namespace {
 
 // Slot g of the reader lives on shard g % N (slot index g / N there), so the
@@ -1161,6 +1163,10 @@ public:
 		if (s.pending) {
 			HIPCK(hipEventSynchronize(s.done));
 			s.pending = false;
+		}
+		if (!s.h_seq) {   // first use of the slot (reserve_ingest_slots, alloc = false)
+			const int rc = ingest_slot_alloc(s);
+			if (rc != VC_OK) return rc;
 		}
 		fill(s, b);
 		return VC_OK;
@@ -1237,9 +1243,9 @@ static int clamp_threads(int n) { return n < 1 ? 1 : (n > 64 ? 64 : n); }
 // one piece each: sequence bytes at about half a FASTQ piece, growing on
 // demand for FASTA), rounded up to a multiple of the shards and spread over
 // them.  Returns the reader's slot count (> 0) or an error (< 0).
-static int reserve_ingest_slots(vc_ctx *c, size_t slots);
+static int reserve_ingest_slots(vc_ctx *c, size_t slots, bool alloc);
 
-static int reserve_ingest(vc_ctx *c, int threads)
+static int reserve_ingest(vc_ctx *c, int threads, bool alloc)
 {
 	const int N = n_shards(c);
 	const char *e = getenv("VAFC_INGEST_SLOTS");   // A/B knob: the reader's slot count (> threads)
@@ -1248,13 +1254,23 @@ static int reserve_ingest(vc_ctx *c, int threads)
 	for (int i = 0; i < N; ++i) {
 		vc_ctx *sh = shard_at(c, i);
 		HIPCK(hipSetDevice(sh->dev));
-		int rc = reserve_ingest_slots(sh, (size_t)(slots / N));
+		int rc = reserve_ingest_slots(sh, (size_t)(slots / N), alloc);
 		if (rc != VC_OK) return rc;
 	}
 	return slots;
 }
 
-static int reserve_ingest_slots(vc_ctx *c, size_t slots)
+// One slot's buffers.  FASTQ: at most half of a piece's records' text is
+// sequence (the quality line is as long); FASTA and long records grow the slot.
+static int ingest_slot_alloc(Slot &s)
+{
+	return slot_reserve(s, VC_PIECE_BYTES / 2 + ((size_t)256 << 10), VC_PIECE_BYTES / 256 + 4096);
+}
+
+// alloc = false: only the slot records and their events; each slot's buffers
+// are then allocated by the worker that first fills it (DeviceSink::acquire),
+// so pinning them overlaps the other workers' parsing instead of preceding it.
+static int reserve_ingest_slots(vc_ctx *c, size_t slots, bool alloc)
 {
 	if (c->islot.size() < slots) {
 		HIPCK(hipStreamSynchronize(c->st));
@@ -1263,12 +1279,10 @@ static int reserve_ingest_slots(vc_ctx *c, size_t slots)
 		for (size_t i = old; i < slots; ++i)
 			HIPCK(hipEventCreateWithFlags(&c->islot[i].done, hipEventDisableTiming));
 	}
-	for (size_t i = 0; i < slots; ++i) {
+	for (size_t i = 0; alloc && i < slots; ++i) {
 		Slot &s = c->islot[i];
 		if (s.h_seq) continue;
-		// FASTQ: at most half of a piece's records' text is sequence (the
-		// quality line is as long); FASTA and long records grow the slot
-		int rc = slot_reserve(s, VC_PIECE_BYTES / 2 + ((size_t)256 << 10), VC_PIECE_BYTES / 256 + 4096);
+		int rc = ingest_slot_alloc(s);
 		if (rc != VC_OK) return rc;
 	}
 	return VC_OK;
@@ -1277,7 +1291,7 @@ static int reserve_ingest_slots(vc_ctx *c, size_t slots)
 extern "C" int vc_reserve_file_ingest(vc_ctx *c, int n_threads)
 {
 	if (!c) return VC_EINVAL;
-	const int rc = reserve_ingest(c, clamp_threads(n_threads));
+	const int rc = reserve_ingest(c, clamp_threads(n_threads), true);
 	return rc < 0 ? rc : VC_OK;
 }
 
@@ -1285,7 +1299,7 @@ static int count_file_parallel(vc_ctx *c, int fd, uint64_t size, int block_bases
                                vc_file_stats &st)
 {
 	const int threads = clamp_threads(n_threads);
-	const int slots = reserve_ingest(c, threads);
+	const int slots = reserve_ingest(c, threads, false);
 	if (slots < 0) return slots;
 	DeviceSink sink(c);
 	const char *pe = getenv("VAFC_INGEST_PIECE");          // test knob: piece size in bytes
@@ -1298,7 +1312,7 @@ static int count_file_parallel(vc_ctx *c, int fd, uint64_t size, int block_bases
 static int count_file_gzip(vc_ctx *c, VcGzParallel *g, int block_bases, int n_threads, vc_file_stats &st)
 {
 	const int parsers = vc_gz_parse_threads(clamp_threads(n_threads));
-	const int slots = reserve_ingest(c, parsers);
+	const int slots = reserve_ingest(c, parsers, false);
 	if (slots < 0) return slots;
 	DeviceSink sink(c);
 	const char *pe = getenv("VAFC_INGEST_PIECE");          // test knob: piece size in bytes
