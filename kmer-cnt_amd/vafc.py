@@ -349,6 +349,11 @@ class KmerMap:
         _ck(lib().vc_count_device(self._h, P(seq_ptr), seq_bytes, P(offs_ptr), P(lens_ptr),
                                   n_reads, P(stream) if stream else None), "vc_count_device")
 
+    def reserve_file_ingest(self, n_thread: int = 4) -> None:
+        """Allocate count_file's parallel-reader buffers now (vc_reserve_file_ingest);
+        without it they are allocated by the reader's workers on first use."""
+        _ck(lib().vc_reserve_file_ingest(self._h, n_thread), "vc_reserve_file_ingest")
+
     def count_file(self, fn: str, block_size: int = 10_000_000, n_thread: int = 4) -> FileStats:
         st = FileStats()
         rc = lib().vc_count_file(self._h, fn.encode(), block_size, n_thread, C.byref(st))

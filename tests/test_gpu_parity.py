@@ -370,7 +370,9 @@ def test_count_file_equals_oracle_file_pass(tmp_path):
 def test_count_file_parallel_reader_on_fuzzed_input(seed, tmp_path, monkeypatch):
     """vc_count_file's parallel reader (forced onto a small file with tiny
     pieces) on malformed FASTQ/FASTA: counts, bases and k-mers equal the
-    oracle's whole-file pass."""
+    oracle's whole-file pass.  Odd seeds reserve the reader's buffers up
+    front (vc_reserve_file_ingest), even seeds let the workers allocate each
+    slot on first use; seed 3 also runs with three slots for three workers."""
     import re
     import vafc
     import oracle as O
@@ -386,9 +388,13 @@ def test_count_file_parallel_reader_on_fuzzed_input(seed, tmp_path, monkeypatch)
             f.write("chr1\t%d\t%d\trs%d\tA\tC\t%s\t%s\n" % (i, i + 1, i, r[:9], r[1:10]))
     monkeypatch.setenv("VAFC_INGEST_MIN", "0")
     monkeypatch.setenv("VAFC_INGEST_PIECE", str(37 + 101 * seed))
+    if seed == 3:
+        monkeypatch.setenv("VAFC_INGEST_SLOTS", "4")
     for b in (10_000_000, 50):
         db = vafc.load_patterns(pat)
         m = vafc.create_combined_kmer_map(db, 9)
+        if seed % 2:
+            m.reserve_file_ingest(3)
         st = m.count_file(fq, b, 3)
         got, km = m.finish()
         orc = O.Oracle(9, pattern_fn=pat)
