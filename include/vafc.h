@@ -204,7 +204,7 @@ int vc_count_file(vc_ctx *ctx, const char *path, int block_bases, int n_threads,
                   vc_file_stats *st);
 
 /* Optional: allocate vc_count_file's parallel-reader buffers for n_threads
- * reader threads now (pinned host + device memory, about 10 MB per thread),
+ * reader threads now (pinned host + device memory, about 20 MB per thread),
  * so that a later vc_count_file does not pay for the allocation.  Without
  * it, vc_count_file's workers allocate each buffer on its first use, while
  * the other workers parse.  The CLI does not call it (VAFC_RESERVE=1 makes

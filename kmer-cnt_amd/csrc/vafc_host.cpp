@@ -1239,7 +1239,7 @@ private:
 
 static int clamp_threads(int n) { return n < 1 ? 1 : (n > 64 ? 64 : n); }
 
-// Pinned + device buffers of the parallel reader's slots (threads + 2 slots of
+// Pinned + device buffers of the parallel reader's slots (2 x threads slots of
 // one piece each: sequence bytes at about half a FASTQ piece, growing on
 // demand for FASTA), rounded up to a multiple of the shards and spread over
 // them.  Returns the reader's slot count (> 0) or an error (< 0).
@@ -1248,8 +1248,11 @@ static int reserve_ingest_slots(vc_ctx *c, size_t slots, bool alloc);
 static int reserve_ingest(vc_ctx *c, int threads, bool alloc)
 {
 	const int N = n_shards(c);
+	// two slots per worker: a piece that finishes late holds back only its
+	// own slot while the others parse ahead (threads + 2 slots left the
+	// workers waiting for slots 2-3x as long: profiles/r04l_slots_ab.json)
 	const char *e = getenv("VAFC_INGEST_SLOTS");   // A/B knob: the reader's slot count (> threads)
-	const int want = e && atoi(e) > threads ? atoi(e) : threads + 2;
+	const int want = e && atoi(e) > threads ? atoi(e) : (threads < 2 ? threads + 2 : 2 * threads);
 	const int slots = (want + N - 1) / N * N;
 	for (int i = 0; i < N; ++i) {
 		vc_ctx *sh = shard_at(c, i);
