@@ -372,7 +372,8 @@ def test_count_file_parallel_reader_on_fuzzed_input(seed, tmp_path, monkeypatch)
     pieces) on malformed FASTQ/FASTA: counts, bases and k-mers equal the
     oracle's whole-file pass.  Odd seeds reserve the reader's buffers up
     front (vc_reserve_file_ingest), even seeds let the workers allocate each
-    slot on first use; seed 3 also runs with three slots for three workers."""
+    slot on first use; seed 3 also runs with four slots for three workers,
+    seed 2 reads the file through a read-only mapping (VAFC_MMAP=1)."""
     import re
     import vafc
     import oracle as O
@@ -390,6 +391,8 @@ def test_count_file_parallel_reader_on_fuzzed_input(seed, tmp_path, monkeypatch)
     monkeypatch.setenv("VAFC_INGEST_PIECE", str(37 + 101 * seed))
     if seed == 3:
         monkeypatch.setenv("VAFC_INGEST_SLOTS", "4")
+    if seed == 2:
+        monkeypatch.setenv("VAFC_MMAP", "1")   # the mapped-file source, parsed in place
     for b in (10_000_000, 50):
         db = vafc.load_patterns(pat)
         m = vafc.create_combined_kmer_map(db, 9)
