@@ -81,17 +81,16 @@ LIMITER_FLANK = ("the roofline is HBM (integer byte work, no MFMA); the kernel r
                  "the flank lookups); an ablation in one process puts 85 % of the time in instruction issue "
                  "(VALU-only variant 4.19 of 4.93 ms), 10 % in the hit path, 4 % in the read loads and 0.6 % in "
                  "the LDS lookups (their bank conflicts, 0.70 of the LDS cycles, hide behind the other waves); "
-                 "HBM requests are 1.47x the algorithmic bytes (boundary lines shared by neighbouring reads "
-                 "fetched twice), not the limit; DESIGN.md sections 3.1.1-3.1.2, "
-                 "profiles/r04f_final_c2_pmc_counters.json, profiles/r04c_ablation_time.log")
+                 "HBM requests are 1.47x the algorithmic bytes (the waves' live read lines, 4.9 MB per XCD, "
+                 "overflow its 4 MB L2 and are fetched again), not the limit; DESIGN.md sections 3.1.1-3.1.2, "
+                 "profiles/r04j_final_c2_pmc_counters.json, profiles/r04c_ablation_time.log")
 LIMITER_LARGE_PANEL = ("the roofline is HBM (integer byte work, no MFMA); the large-panel kernel runs far below "
                        "it, bound by VALU issue and the texture-address (TA) rate of its gathers: 9.3 % of "
                        "windows pass the 144 KiB LDS Bloom filter (about 6 % is that size's information limit "
                        "for 200k SNP pairs), each pass is a hit-loop trip and one lane of a random gather into "
                        "the L2-resident second-level filter; 23.6 VALU per base (5.5 G per launch, ~0.8 of the "
-                       "kernel time at ~4 cycles each), TA busy ~0.5 of the cycles (round-3 closing PMC of the "
-                       "same kernel; round 4 changed no C5 code: 11.44 ms, profiles/r04f_final_c5_kernel_timed.json); "
-                       "DESIGN.md section 3.1 (large panels), profiles/r03_close2_c5_pmc_counters.json")
+                       "kernel time at ~4 cycles each), TA busy ~0.5 of the cycles (3.66 G over 256 CUs); "
+                       "DESIGN.md section 3.1 (large panels), profiles/r04j_final_c5_pmc_counters.json")
 
 
 def cli_run(binary, pat, fq, threads, out, k, env=None, timeout=900):
