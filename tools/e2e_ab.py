@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--gzip", action="store_true", help="pigz-shaped gzip level 1 (bench.py's e2e file)")
     ap.add_argument("--gzip-single", action="store_true",
                     help="one plain zlib level-1 deflate stream (gzip -1's shape: no sync-flushed pieces)")
+    ap.add_argument("--bgzf", action="store_true",
+                    help="BGZF-shaped gzip (bgzip's layout: independent members of 64 KiB of text, level 1)")
     ap.add_argument("--host-parse", action="store_true",
                     help="also time the parallel reader alone (vc_scan_file_parallel, no GPU) under each variant's env")
     ap.add_argument("variants", nargs="+")
@@ -73,6 +75,19 @@ def main():
         path = fq + ".gz"
         bench.gzip_level1(fq, path, a.threads)
         os.unlink(fq)
+    elif a.bgzf:
+        import struct
+        import zlib
+        path = fq + ".gz"
+        with open(fq, "rb") as f, open(path, "wb") as g:
+            for b in iter(lambda: f.read(65280), b""):
+                c = zlib.compressobj(1, zlib.DEFLATED, -15)
+                body = c.compress(b) + c.flush()
+                # FEXTRA with the BC subfield holding the member size - 1 (SAM spec, BGZF)
+                hdr = b"\x1f\x8b\x08\x04" + b"\x00\x00\x00\x00" + b"\x00\xff" + struct.pack("<H", 6) + b"BC" + \
+                    struct.pack("<HH", 2, 18 + len(body) + 8 - 1)
+                g.write(hdr + body + struct.pack("<II", zlib.crc32(b) & 0xFFFFFFFF, len(b) & 0xFFFFFFFF))
+        os.unlink(fq)
     elif a.gzip_single:
         import gzip
         path = fq + ".gz"
@@ -95,7 +110,8 @@ def main():
         specs.append((name, os.path.join(ROOT, parts[0]), env, thr))
     out = {"workload": "%dM x %d bp reads of the C2 stream, %s, -t %d" % (
         R // 1_000_000, L, "gzip level 1, pigz-shaped" if a.gzip else
-        ("gzip level 1, one stream (gzip -1 shape)" if a.gzip_single else "plain FASTQ"), a.threads), "runs": {}}
+        ("gzip level 1, one stream (gzip -1 shape)" if a.gzip_single else
+         ("BGZF, 64 KiB members, level 1" if a.bgzf else "plain FASTQ")), a.threads), "runs": {}}
     md5s = {}
     for name, cli, env, thr in specs:   # one untimed pass each: the first pass over a fresh file is slow
         bench.cli_run(cli, pat, path, thr, os.path.join(tmp, "warm.vaf"), 21, env=env, timeout=300)
