@@ -679,8 +679,9 @@ extern "C" int vc_scan_file_parallel(const char *path, int k, int block_bases, i
 		close(fd);
 		return VC_EINVAL;
 	}
-	HostSink sink(n_threads + 2, piece_bytes, seq_out, seq_cap, lens_out, lens_cap);
-	const int rc = vc_ingest_plain(fd, (uint64_t)sb.st_size, k, block_bases, n_threads, n_threads + 2,
+	const int slots = n_threads < 2 ? n_threads + 2 : 2 * n_threads;   // as vc_count_file's reader
+	HostSink sink(slots, piece_bytes, seq_out, seq_cap, lens_out, lens_cap);
+	const int rc = vc_ingest_plain(fd, (uint64_t)sb.st_size, k, block_bases, n_threads, slots,
 	                               piece_bytes, sink, local);
 	close(fd);
 	local.seconds = mono_now() - t0;
