@@ -64,11 +64,19 @@ static int newlines4_memchr(const uint8_t *p, const uint8_t *e, const uint8_t **
 	return n;
 }
 
-// VAFC_NL_SCAN=memchr: one memchr per line (the A/B baseline)
-static int (*const newlines4)(const uint8_t *, const uint8_t *, const uint8_t **) =
-	getenv("VAFC_NL_SCAN") && !strcmp(getenv("VAFC_NL_SCAN"), "memchr") ? newlines4_memchr
-	: __builtin_cpu_supports("avx2")                                     ? newlines4_avx2
-	                                                                     : newlines4_sse2;
+typedef int (*Newlines4Fn)(const uint8_t *, const uint8_t *, const uint8_t **);
+
+// VAFC_NL_SCAN=memchr: one memchr per line (the A/B baseline).  Chosen while
+// the library's constructors run, so the CPU model is initialised first
+// (__builtin_cpu_supports may otherwise read it before libgcc has).
+static Newlines4Fn pick_newlines4()
+{
+	__builtin_cpu_init();
+	const char *e = getenv("VAFC_NL_SCAN");
+	if (e && !strcmp(e, "memchr")) return newlines4_memchr;
+	return __builtin_cpu_supports("avx2") ? newlines4_avx2 : newlines4_sse2;
+}
+static const Newlines4Fn newlines4 = pick_newlines4();
 
 bool VcFastqReader::open(const char *path, size_t window)
 {
