@@ -694,8 +694,10 @@ def main():
             "cpu_baseline": cpu,
             "parity_vs_reference_on_sample": parity,
             "parity_note": ("the product's .vaf on the first %d reads == the reference's (md5)" % n if world == 1 else
-                            "all %d ranks count the first %d reads of the stream, RCCL all-reduce; == %d x the "
-                            "reference's counts on that sample (u32)" % (world, n, world)),
+                            "all %d ranks count the first %d reads of the stream, %s all-reduce; == %d x the "
+                            "reference's counts on that sample (u32)"
+                            % (world, n, "RCCL" if os.environ.get("VAFC_DIST_BACKEND", "nccl") == "nccl" else
+                               os.environ.get("VAFC_DIST_BACKEND"), world)),
             "build_id": vafc.tree_build_id(),
             "e2e": e2e,
         }
