@@ -1,36 +1,46 @@
 #!/usr/bin/env python3
 """bench.py -- headline benchmark of the MI355X vaf-counter hot path.
 
-Metric (BASELINE.json): Mbases/sec (+ k-mers/sec) on 150 bp FASTQ, k=21.
-Workload (configs[1], "C2"): per GPU 100M synthetic 150 bp reads against the
+Metric (BASELINE.json): Mbases/sec (+ k-mers/sec) on 150 bp FASTQ, k=21, as
+the reference defines it: bases / counting-phase wall clock
+(vaf-counter.c:646-651,707), FASTQ parse, PCIe and kernels included.
+Workload (configs[1], "C2"): 100M synthetic 150 bp reads against the
 SNP_GRCh38_hg38_wChr panel (20,849 ACGT patterns), generated on the device by
-the same counter-based generator as kmer-cnt_amd/vafc_synth.py, resident in
-HBM before the timed region.  --config c3 (k = 31, 100M pairs), c5 (200k-SNP
-panel) and c4 (1B reads in total, split over the ranks: strong scaling) are
-the other BASELINE.json configs.
+the counter-based generator of kmer-cnt_amd/vafc_synth.py and written once as
+one 4-line FASTQ file (31.5 GB) into the page cache (/dev/shm).
 
-One step = one pass of the hot path over the whole batch: zero the counts,
-decode + extract + filter + probe + count every read (vc_count_device), and --
-with N > 1 -- the RCCL all-reduce of the uint32 count vector and the k-mer
-tally (torch.distributed "nccl" backend), all enqueued on one stream with no
-host synchronisation inside the step.  `value` is kernel-side throughput on
-HBM-resident reads; it excludes FASTQ parsing and PCIe.
+One step = one pass of the product over the whole file: every rank counts
+its byte range of the file (vc_count_file_range, the torchrun driver's split,
+kmer-cnt_amd/vafc_dist.py) into its GPU's counts, then ONE all-reduce of the
+uint32 counts and the k-mer tally (RCCL with the "nccl" backend).  W untimed
+steps, then K timed steps between a barrier + torch.cuda.synchronize() on
+both sides; the time is the maximum over ranks.  value = bases of the file x
+K / that time.  The file is fixed, so N GPUs split the same work ("scaling":
+"strong").  `python bench.py --gpus N` starts N rank processes itself (one per
+GPU, before any GPU call) unless it runs under torchrun already, whose
+WORLD_SIZE must then equal N.
 
 Also reported:
-  roofline      the counting kernels' algorithmic bytes (1 B/base
-                + 8 B/read; the layout's 12 B/read beside it) / their event-timed duration,
-                against 8 TB/s HBM3E; traffic from a committed rocprofv3 PMC
-                summary of this workload (profiles/pmc_summary.json) if present.
+  steps_detail  per timed step: wall, the slowest rank's counting seconds and
+                its reader profile (vc_ingest_profile: main-thread waits,
+                H2D submits, parse and slot waits), so a slow step names its
+                phase.
+  roofline      the counting kernel on HBM-resident reads (1 B
+                per base + 8 B per read; the layout's 12 B/read beside it) /
+                its HIP-event-timed duration, against 8 TB/s HBM3E; traffic
+                from a committed rocprofv3 PMC summary (profiles/pmc_summary.json).
+                Its kernel-side Mbases/s is `kernel_value`.
   cpu_baseline  the REAL reference vaf-counter (oracle/_ref, compiled from the
-                reference sources) on a bounded sample of the same reads written
-                as FASTQ, timed by its own -v "Speed" line; median of 3 at
-                -t 1 / 4 / 16 / nproc, the best median.
-  parity        the product's .vaf on that sample vs the reference's (md5).
-  e2e           the metric as the reference defines it (bases / counting-phase
-                wall clock, vaf-counter.c:646-651,707): the drop-in CLI on a
-                page-cached 16M-read FASTQ written on the box, plain and
-                gzip level 1, parse + PCIe + kernels + reduce included; the
-                reference on the same file for .vaf parity.
+                reference sources) on a bounded sample of the same reads
+                written as FASTQ, timed by its own -v "Speed" line; median of
+                3 at -t 1 / 4 / 16 / nproc, the best median.
+  parity        the product's .vaf on that sample vs the reference's (md5);
+                the whole file's counts vs the product's vc_count_device on
+                the same HBM reads (self-consistency at full size).
+  cli           (N = 1) the drop-in CLI binary on the same file, plain and
+                gzip level 1, its own -v Speed line, with a stage roofline.
+--config c3 / c4 / c5 (the other BASELINE.json configs) measure the counting
+kernel on HBM-resident reads only (value = kernel-side Mbases/s).
 """
 import argparse
 import hashlib
@@ -236,9 +246,11 @@ def gzip_level1(src, dst, threads, chunk=16 << 20):
     return os.path.getsize(dst)
 
 
-def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None, dev=None, device_vaf=None, kernel_s=None):
-    """The drop-in CLI end to end on a page-cached FASTQ of the first n_reads
-    HBM reads (plain, gzip), median of 3 runs each.
+def cli_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None, dev=None, device_vaf=None, kernel_s=None,
+            fq=None):
+    """The drop-in CLI binary end to end on a page-cached FASTQ of the first
+    n_reads HBM reads (plain, gzip), median of VAFC_CLI_RUNS (3) runs each;
+    fq: that FASTQ when the caller wrote it already (kept).
 
     device_vaf: md5 of the .vaf that count_device gives on the same HBM reads
     -- the CLI's .vaf on the file must equal it (a full-size bit-exact check;
@@ -249,16 +261,20 @@ def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None, dev=None, device_
     import vafc
     t = cpu_share(len(devices) if devices else 1)
     est = n_reads * (2 * L + 16)
-    work = scratch_dir(est * 1.25, tmp)
-    fq = os.path.join(work, "e2e.fq")
-    gz = fq + ".gz"
-    t0 = time.time()
-    write_fastq_from_device(d_seq, n_reads, L, fq, threads=t)
+    own_fq = fq is None
+    if own_fq:
+        work = scratch_dir(est * 1.25, tmp)
+        fq = os.path.join(work, "e2e.fq")
+        t0 = time.time()
+        write_fastq_from_device(d_seq, n_reads, L, fq, threads=t)
+        log("cli: %d reads as FASTQ in %s in %.1fs" % (n_reads, work, time.time() - t0))
+    else:
+        work = os.path.dirname(fq)
+    gz = os.path.join(work, "cli.fq.gz")
     fq_bytes = os.path.getsize(fq)
-    log("e2e: %d reads as FASTQ (%.2f GB) in %s in %.1fs" % (n_reads, fq_bytes / 1e9, work, time.time() - t0))
     t0 = time.time()
     gz_bytes = gzip_level1(fq, gz, t)
-    log("e2e: gzip level 1 (%.2f GB) in %.1fs" % (gz_bytes / 1e9, time.time() - t0))
+    log("cli: gzip level 1 (%.2f GB) in %.1fs" % (gz_bytes / 1e9, time.time() - t0))
     out = {"workload": "%dM x %d bp reads (%.2f Gbases) of this workload as 4-line FASTQ (%.2f GB), "
                        "page-cached (%s); k=%d, same panel" % (
                            n_reads // 1_000_000, L, n_reads * L / 1e9, fq_bytes / 1e9,
@@ -279,7 +295,7 @@ def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None, dev=None, device_
                             "one shard per GPU, one RCCL reduce of the counts before the .vaf is written"
                             % len(devices))
     vafs = {}
-    n_runs = int(os.environ.get("VAFC_E2E_RUNS", "5"))
+    n_runs = int(os.environ.get("VAFC_CLI_RUNS", "3"))
     for name, path in (("plain", fq), ("gzip", gz)):
         # one untimed run first: the first pass over a freshly written 31.5 GB
         # file ran at half speed or less on every box (profiles/r04c_n8_projection.json,
@@ -292,7 +308,7 @@ def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None, dev=None, device_
             # leg after 3 minutes instead of holding the whole bench line back
             r = cli_run(PRODUCT_CLI, pat, path, t, o, k, env=env, timeout=180)
             runs.append(r)
-            log("e2e %s -t %d (run %d): %.1f Mbases/s counting phase, %.2fs process" %
+            log("cli %s -t %d (run %d): %.1f Mbases/s counting phase, %.2fs process" %
                 (name, t, rep + 1, r["mbases"], r["wall"]))
         vafs[name] = md5(o)
         srt = sorted(runs, key=lambda r: r["mbases"])
@@ -356,7 +372,7 @@ def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None, dev=None, device_
                           "limiter": max(stages, key=stages.get)}
         out["roofline"] = roof
     except Exception as e:  # never hide the measured line
-        log("e2e roofline failed: %r" % (e,))
+        log("cli roofline failed: %r" % (e,))
     if device_vaf is not None:
         out["parity_vs_count_device_full_size"] = vafs["plain"] == device_vaf and vafs["gzip"] == device_vaf
         out["parity_full_size_note"] = ("self-consistency, not reference parity: the CLI's .vaf on the whole "
@@ -371,38 +387,245 @@ def e2e_leg(d_seq, L, k, pat, tmp, n_reads, cpu, devices=None, dev=None, device_
         r = cli_run(PRODUCT_CLI, pat, fq, cpu_share(), o, k, env=env1)
         out["single_gpu_same_file"] = {"value": r["mbases"], "unit": "Mbases/sec", "threads": cpu_share()}
         out["parity_vs_single_gpu"] = vafs["plain"] == md5(o) and vafs["gzip"] == vafs["plain"]
-    for f in (fq, gz):
-        os.unlink(f)
-    if work != tmp:
-        shutil.rmtree(work, ignore_errors=True)
+    os.unlink(gz)
+    if own_fq:
+        os.unlink(fq)
+        if work != tmp:
+            shutil.rmtree(work, ignore_errors=True)
     return out
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(argv, n, script=None):
+    """`--gpus N` outside torchrun: N rank processes of this script, one per
+    GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1),
+    started before this process touches the GPU.  Rank 0 prints the JSON line
+    (its stdout is ours).  Returns 0, or the exit status of the first rank to
+    fail (the others are then stopped)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    alive = set(range(n))
+    while alive:
+        for r in sorted(alive):
+            x = procs[r].poll()
+            if x is None:
+                continue
+            alive.discard(r)
+            if x != 0 and rc == 0:
+                rc = x if x > 0 else 1
+                log("rank %d exited with %d: stopping the other ranks" % (r, x))
+                for o in alive:
+                    procs[o].terminate()
+        time.sleep(0.1)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def rank_threads(world):
+    """Reader threads per rank: the CPU share of one GPU (16 on the GPU pool),
+    no more than the affinity mask or the cgroup's CPU quota split over the
+    ranks on this node."""
+    n = cpu_share(1)
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    n = min(n, max(1, aff // world))
+    q = cgroup_cpu_max()
+    if q and not q.startswith("max"):
+        try:
+            quota, period = (int(x) for x in q.split()[:2])
+            n = min(n, max(1, quota // period // world))
+        except ValueError:
+            pass
+    return max(1, n)
+
+
+def kernel_leg(kmap, d_seq, d_offs, d_lens, R, L, steps, warmup, world, dist, counts, tally):
+    """The counting kernel on HBM-resident reads: `warmup` + `steps` launches
+    of vc_count_device over this rank's R reads (N > 1: plus the RCCL
+    all-reduce of the counts), all on torch's current stream with no host
+    synchronisation inside; returns (wall seconds of the timed launches, max
+    over ranks; per-launch kernel ms from HIP events)."""
+    import torch
+    kmap.bind_outputs(counts.data_ptr(), tally.data_ptr())
+    kmap.set_timing(True)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        counts.zero_()
+        tally.zero_()
+        kmap.count_device(d_seq.data_ptr(), R * L, d_offs.data_ptr(), d_lens.data_ptr(), R, stream)
+        if world > 1:
+            for x in [dist.all_reduce(counts, async_op=True), dist.all_reduce(tally, async_op=True)]:
+                x.wait()
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+        kernel_ms.append(kmap.kernel_ms())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=counts.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kmap.set_timing(False)
+    return elapsed, kernel_ms
+
+
+def headline_leg(kmap, fq, k, steps, warmup, rank, world, dist, cpu_group, dev, n_pat):
+    """The reference's metric on the whole file, every rank counting its byte
+    range (vafc_dist.byte_range, vc_count_file_range) into its GPU, one
+    all-reduce per step; W untimed + K timed steps between barriers and
+    device synchronisations, time = max over ranks.  Returns the e2e dict
+    (rank 0) and the all-reduced counts of the last step (uint32)."""
+    import torch
+    import vafc
+    import vafc_dist as D
+    threads = rank_threads(world)
+    size = os.path.getsize(fq)
+    begin, end = D.byte_range(size, rank, world)
+    counts = torch.zeros(2 * n_pat, dtype=torch.int32, device=dev)
+    tally = torch.zeros(1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    kmap.bind_outputs(counts.data_ptr(), tally.data_ptr())
+    block = 10_000_000            # the reference's default -b
+
+    def step():
+        counts.zero_()
+        tally.zero_()
+        torch.cuda.synchronize()  # the fills (torch's stream) before the count (the map's own stream)
+        a = time.perf_counter()
+        st, ri = kmap.count_file_range(fq, begin, end, block, threads)   # returns with its stream synced
+        c = time.perf_counter() - a
+        prof = vafc.ingest_profile()
+        if world > 1:
+            dist.all_reduce(counts)
+            dist.all_reduce(tally)
+        torch.cuda.synchronize()
+        return st, ri, c, time.perf_counter() - a, prof
+
+    for w in range(warmup):
+        st, ri, c, sw, _ = step()
+        log("rank %d e2e warmup %d: %.3f s (count %.3f s)" % (rank, w + 1, sw, c))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    rec = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st, ri, c, sw, prof = step()
+        rec.append((sw, c, prof))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    bases, seqs, km = int(st.bases), int(st.seqs), int(tally.item())
+    info = (int(ri.first), int(ri.next), int(ri.errs), int(ri.stopped))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        v = torch.tensor([bases, seqs], dtype=torch.int64, device=dev)
+        dist.all_reduce(v)
+        bases, seqs = (int(x) for x in v.tolist())
+        infos = [None] * world
+        recs = [None] * world
+        dist.all_gather_object(infos, info, group=cpu_group)
+        dist.all_gather_object(recs, rec, group=cpu_group)
+    else:
+        infos, recs = [info], [rec]
+    final = counts.cpu().numpy().view(np.uint32).copy()
+    kmap.bind_outputs(0, 0)
+    if rank != 0:
+        return None, final
+    exact = D.chain_holds(infos)
+    per_step = []
+    for i in range(steps):
+        slow = max(range(world), key=lambda r: recs[r][i][1])
+        per_step.append({"ms": round(1e3 * max(recs[r][i][0] for r in range(world)), 1),
+                         "count_ms": round(1e3 * recs[slow][i][1], 1), "slowest_rank": slow,
+                         "reader": recs[slow][i][2]})
+    rates = sorted(bases / (p["ms"] * 1e-3) / 1e6 for p in per_step)
+    med = rates[len(rates) // 2]
+    e2e = {"value": round(bases * steps / elapsed / 1e6, 1), "unit": "Mbases/sec",
+           "kmers_per_sec": round(km * steps / elapsed, 1),
+           "bases": bases, "seqs": seqs, "kmers": km, "file_bytes": size, "threads_per_rank": threads,
+           "ranks": world, "elapsed_s": round(elapsed, 4),
+           "step_mbases": {"min": round(rates[0], 1), "median": round(med, 1), "max": round(rates[-1], 1),
+                           "spread": round((rates[-1] - rates[0]) / med, 3)},
+           "split_exact": exact, "ranges": [list(x) for x in infos],
+           "steps_detail": per_step,
+           "timer": "per rank: zero the counts, vc_count_file_range over its byte range (first file open to "
+                    "its counts final on the GPU: parse, pinned staging, H2D, kernels), then the all-reduce; "
+                    "K steps between barriers, max over ranks -- the reference's counting-phase clock "
+                    "(vaf-counter.c:646-651,707) plus the reduction its single process does not need"}
+    if not exact:
+        log("e2e: the ranks' byte ranges did not chain (%s): counts not exact" % (infos,))
+    return e2e, final
 
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=10, help="timed steps (passes over the file; c3-c5: launches)")
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--reads", type=int, default=None, help="reads per GPU (c4: in total)")
+    ap.add_argument("--reads", type=int, default=None, help="reads per GPU (c2: of the file; c4: in total)")
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--k", type=int, default=21)
     ap.add_argument("--f-snp", type=float, default=0.01)
     ap.add_argument("--panel", default="grch38", choices=["grch38", "syn200k"])
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
-                    help="BASELINE.json configs: c2 (default, the headline: k=21, 100M reads per GPU), "
+                    help="BASELINE.json configs: c2 (default, the headline: k=21, 100M reads as FASTQ), "
                          "c3 (k=31, 100M pairs = 200M reads of 150 bp), c4 (1B reads in total split over "
-                         "the GPUs: strong scaling), c5 (200k-SNP synthetic panel)")
+                         "the GPUs), c5 (200k-SNP synthetic panel); c3-c5: the kernel on HBM-resident reads")
+    ap.add_argument("--kernel-steps", type=int, default=10, help="c2: timed kernel launches for the roofline")
     ap.add_argument("--cpu-reads", type=int, default=2_000_000, help="CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline timings (the parity sample still runs)")
     ap.add_argument("--no-parity", action="store_true", help="skip the live parity sample too")
-    ap.add_argument("--e2e-reads", type=int, default=None,
-                    help="reads of the end-to-end FASTQ (default: all of the workload's reads on rank 0)")
-    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-cli", action="store_true", help="skip the drop-in CLI binary leg (N = 1)")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="c2 without the FASTQ file: value = the kernel on HBM-resident reads (profiling runs)")
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(sys.argv[1:], args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        log("--gpus %d but WORLD_SIZE is %d: refusing to report one for the other" % (args.gpus, world))
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    strong = args.config == "c4"
+    strong_kernel = args.config == "c4"
+    headline = args.config == "c2" and not args.no_e2e
     if args.config == "c3":
         args.k = 31
         R = 2 * (args.reads or 100_000_000)
@@ -422,19 +645,16 @@ def main():
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    # Every torch op and every vafc launch of this process run on torch's
-    # default stream: its handle 0 is HIP's null stream, which vc_count_device
-    # takes as such (include/vafc.h; the round-3 ABI read 0 as the counter's
-    # own stream, and a zero-fill on torch's default stream raced with the
-    # count, profiles/r03_rank1_parity_race.log).
+    backend = os.environ.get("VAFC_DIST_BACKEND", "nccl")
+    cpu_group = None
     if world > 1:
-        backend = os.environ.get("VAFC_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-        # host-side group for waiting while rank 0 runs the e2e leg on every
-        # GPU (a gloo barrier does not keep an RCCL kernel spinning on them)
+        # host-side group: file names, per-step records, and waiting while rank
+        # 0 writes the file or runs the reference (a gloo barrier does not keep
+        # an RCCL kernel spinning on the GPUs)
         cpu_group = dist.new_group(backend="gloo")
     import vafc
     import vafc_synth as S
@@ -447,13 +667,17 @@ def main():
     pat = os.path.join(tmp, "patterns.txt")
     panel.write_patterns(pat, args.k)
     db = vafc.load_patterns(pat)
-    kmap = vafc.create_combined_kmer_map(db, args.k, device=local)
+    keys, vals, coll = db.keys(args.k)
+    if coll and rank == 0:
+        log("%d k-mer collisions in the panel (the reference warns the same)" % coll)
+    kmap = vafc.KmerMap(args.k, keys, vals, db.n, local)
     tinfo = kmap.table_info()
     n_pat = db.n
 
-    # ---- synthetic reads, resident in HBM (rank r: reads r*R0 .. of the stream)
+    # ---- synthetic reads, resident in HBM (rank r: reads r*R .. of the stream;
+    # c2: the file is rank 0's reads, every rank counts a byte range of it)
     L = args.read_len
-    if strong:
+    if strong_kernel:
         base, extra = divmod(args.reads or 1_000_000_000, world)
         first = rank * base + min(rank, extra)
     else:
@@ -471,60 +695,22 @@ def main():
     torch.cuda.synchronize()
     log("rank %d: %d reads x %d bp generated in HBM in %.2fs" % (rank, R, L, time.time() - t0))
 
+    # ---- the counting kernel on HBM-resident reads (roofline)
     counts = torch.zeros(2 * n_pat, dtype=torch.int32, device=dev)
     tally = torch.zeros(1, dtype=torch.int64, device=dev)
-    kmap.bind_outputs(counts.data_ptr(), tally.data_ptr())
-    kmap.set_timing(True)
-    stream = torch.cuda.current_stream().cuda_stream
-
-    def step():
-        # everything on torch's current stream: zero, count, then the RCCL
-        # all-reduces (their stream waits on this one) -- no host sync
-        counts.zero_()
-        tally.zero_()
-        kmap.count_device(d_seq.data_ptr(), R * L, d_offs.data_ptr(), d_lens.data_ptr(), R, stream)
-        if world > 1:
-            w = [dist.all_reduce(counts, async_op=True), dist.all_reduce(tally, async_op=True)]
-            for x in w:
-                x.wait()
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    kernel_ms = []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        kernel_ms.append(kmap.kernel_ms())
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    k_steps, k_warm = (args.kernel_steps, 2) if headline else (args.steps, args.warmup)
+    k_elapsed, kernel_ms = kernel_leg(kmap, d_seq, d_offs, d_lens, R, L, k_steps, k_warm, world, dist, counts, tally)
     reads_total = R
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
         n = torch.tensor([R], dtype=torch.int64, device=dev)
         dist.all_reduce(n)
         reads_total = int(n.item())
-
-    kmers_total = int(tally.item())           # after the all-reduce: all ranks' k-mers
-    bases_total = reads_total * L
-    ms_step = elapsed / args.steps * 1e3
-    value = bases_total * args.steps / elapsed / 1e6
-    kmer_rate = kmers_total * args.steps / elapsed
-
-    # ---- roofline of the counting kernels (this rank's launch).  Algorithmic
-    # bytes as SURVEY.md section 8(d) defines them: 1 B per base + 8 B per read
-    # (one u64 offset, or a u32 offset + length).  The kernel's input layout
-    # reads 12 B per read (u64 offset + u32 length); that figure is reported
-    # beside it (layout_bytes_per_launch, frac_layout).
+    k_value = reads_total * L * k_steps / k_elapsed / 1e6
+    k_kmer_rate = int(tally.item()) * k_steps / k_elapsed
     k_ms = float(np.mean(kernel_ms))
+    # algorithmic bytes as SURVEY.md section 8(d) defines them: 1 B per base +
+    # 8 B per read (one u64 offset, or a u32 offset + length); the kernel's
+    # input layout reads 12 B per read (u64 offset + u32 length), reported beside it
     alg_bytes = R * L * 1 + R * 8
     layout_bytes = R * L * 1 + R * 12
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
@@ -548,8 +734,8 @@ def main():
     # baseline) on the sample; the other ranks wait on the gloo barrier.
     cpu = None
     parity = None
-    e2e = None
     n = min(args.cpu_reads, R)
+    stream = torch.cuda.current_stream().cuda_stream
     if not args.no_parity and n > 0:
         if first == 0:
             p_seq, p_offs, p_lens = d_seq, d_offs, d_lens
@@ -558,12 +744,10 @@ def main():
             p_offs = torch.empty(n, dtype=torch.int64, device=dev)
             p_lens = torch.empty(n, dtype=torch.int32, device=dev)
             vafc.synth_reads(p_seq.data_ptr(), p_offs.data_ptr(), p_lens.data_ptr(), 0, n, L,
-                             S.READ_SEED_R1, args.f_snp, win.data_ptr(), dos.data_ptr(), panel.n,
-                             torch.cuda.current_stream().cuda_stream)
+                             S.READ_SEED_R1, args.f_snp, win.data_ptr(), dos.data_ptr(), panel.n, stream)
         par_counts = torch.zeros(2 * n_pat, dtype=torch.int32, device=dev)
         par_tally = torch.zeros(1, dtype=torch.int64, device=dev)
         kmap.bind_outputs(par_counts.data_ptr(), par_tally.data_ptr())
-        kmap.set_timing(False)
         kmap.count_device(p_seq.data_ptr(), n * L, p_offs.data_ptr(), p_lens.data_ptr(), n, stream)
         torch.cuda.synchronize()
         par_local = par_counts.cpu().numpy().view(np.uint32).copy()
@@ -628,82 +812,137 @@ def main():
                         int((par.astype(np.uint64) != want).sum())))
         except Exception as e:  # the baseline must never hide the measured line
             log("cpu baseline failed: %r" % (e,))
-    if rank == 0 and not args.no_e2e and args.config == "c2":
-        # the reference's own metric on this workload's reads (all R of rank 0's
-        # reads by default); N > 1: one CLI process over all N GPUs (the other
-        # ranks wait at the barrier below)
-        try:
-            ne = min(args.e2e_reads or R, R)
-            kmap.set_timing(True)
+
+    # ---- the headline: the reference's metric on rank 0's reads as one FASTQ
+    e2e = cli = None
+    full_parity = None
+    if headline:
+        fq_path = None
+        work = None
+        if rank == 0:
+            work = scratch_dir(R * (2 * L + 16) * 1.25, tmp)
+            fq_path = os.path.join(work, "c2.fq")
+            t0 = time.time()
+            write_fastq_from_device(d_seq, R, L, fq_path, threads=cpu_share())
+            log("e2e: %d reads as FASTQ (%.2f GB) in %s in %.1fs" % (R, os.path.getsize(fq_path) / 1e9, work,
+                                                                      time.time() - t0))
+        if world > 1:
+            box = [fq_path]
+            dist.broadcast_object_list(box, src=0, group=cpu_group)
+            fq_path = box[0]
+        e2e, e_counts = headline_leg(kmap, fq_path, args.k, args.steps, args.warmup, rank, world, dist,
+                                     cpu_group, dev, n_pat)
+        if rank == 0:
+            # full-size self-consistency: the file's counts (all ranks' ranges,
+            # all-reduced) == vc_count_device over the same HBM reads
             kmap.reset()
-            kmap.count_device(d_seq.data_ptr(), ne * L, d_offs.data_ptr(), d_lens.data_ptr(), ne)
-            ec, _ = kmap.finish()
-            e_ks = kmap.kernel_ms() * 1e-3
-            dev_vaf = os.path.join(tmp, "device_e2e.vaf")
-            db.write_vaf(ec, dev_vaf)
-            e2e = e2e_leg(d_seq, L, args.k, pat, tmp, ne, cpu,
-                          devices=[r % max(torch.cuda.device_count(), 1) for r in range(world)] if world > 1
-                          else None, dev=dev, device_vaf=md5(dev_vaf), kernel_s=e_ks / world)
-        except Exception as e:
-            log("e2e leg failed: %r" % (e,))
-    if world > 1:
+            kmap.count_device(d_seq.data_ptr(), R * L, d_offs.data_ptr(), d_lens.data_ptr(), R)
+            dc, dkm = kmap.finish()
+            full_parity = bool(np.array_equal(dc, e_counts)) and e2e["kmers"] == dkm and e2e["split_exact"]
+            e2e["parity_vs_count_device_full_size"] = full_parity
+            e2e["parity_full_size_note"] = ("self-consistency, not reference parity: the counts of the whole "
+                                            "file over %d rank range(s), all-reduced, equal the product's own "
+                                            "vc_count_device on the same %d HBM reads; the reference itself "
+                                            "is checked on the cpu_baseline sample" % (world, R))
+            if cpu:
+                e2e["vs_cpu_baseline"] = round(e2e["value"] / cpu["value"], 1)
+            if world == 1 and not args.no_cli:
+                try:
+                    dev_vaf = os.path.join(tmp, "device_e2e.vaf")
+                    db.write_vaf(dc, dev_vaf)
+                    cli = cli_leg(d_seq, L, args.k, pat, tmp, R, cpu, dev=dev, device_vaf=md5(dev_vaf),
+                                  kernel_s=k_ms * 1e-3, fq=fq_path)
+                except Exception as e:
+                    log("cli leg failed: %r" % (e,))
+            os.unlink(fq_path)
+            if work != tmp:
+                shutil.rmtree(work, ignore_errors=True)
+        if world > 1:
+            dist.barrier(group=cpu_group)
+    elif world > 1:
         dist.barrier(group=cpu_group)
 
     if rank == 0:
+        data_src = "SNP_GRCh38_hg38_wChr.bed" if args.panel == "grch38" else "a 200k-row synthetic BED"
+        kernel_obj = {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "vc_count_reads_kernel (+ vc_count_long_kernel, empty here)",
+            "limiter": (LIMITER_LARGE_PANEL if tinfo["n_keys"] > 65536 else LIMITER_FLANK),
+            "kernel_ms": round(k_ms, 4),
+            "kernel_launches": k_steps,
+            "kernel_value": round(k_value, 1),
+            "kernel_value_unit": "Mbases/sec on HBM-resident reads (no FASTQ parse, no PCIe)",
+            "kernel_kmers_per_sec": round(k_kmer_rate, 1),
+            "alg_bytes_per_launch": alg_bytes,
+            "alg_bytes_rule": "SURVEY.md 8(d): 1 B/base + 8 B/read",
+            "layout_bytes_per_launch": layout_bytes,
+            "frac_layout": round(layout_bytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        }
+        if headline:
+            value, unit = e2e["value"], "Mbases/sec"
+            ms_step = e2e["elapsed_s"] / args.steps * 1e3
+            kmer_rate = e2e["kmers_per_sec"]
+            data = ("synthetic (counter-based generator, seed 42; patterns from %s, flanks seed 12345), written "
+                    "once as one 4-line FASTQ into the page cache; value = the reference's metric over the whole "
+                    "file (bases / counting wall, vaf-counter.c:646-651,707): parse, pinned staging, PCIe, "
+                    "kernels and the all-reduce inside every step; the kernel alone on HBM-resident reads is "
+                    "roofline.kernel_value" % data_src)
+            workload = ("C2: %dM x %d bp reads as one FASTQ (%.2f GB, page cache), k=%d, %s panel (%d patterns, "
+                        "%d keys), f_snp=%g; %d rank(s), each counting a byte range of the file" % (
+                            R // 1_000_000, L, e2e["file_bytes"] / 1e9, args.k, args.panel, n_pat,
+                            tinfo["n_keys"], args.f_snp, world))
+            scaling = "strong"
+            parallelism = ("dp%d (byte ranges of the file per rank, RCCL all-reduce of uint32 counts + u64 tally)"
+                           % world)
+        else:
+            value, unit = round(k_value, 1), "Mbases/sec"
+            ms_step = k_elapsed / k_steps * 1e3
+            kmer_rate = k_kmer_rate
+            data = ("synthetic (counter-based generator, seed 42; patterns from %s, flanks seed 12345), resident "
+                    "in HBM: value is the kernel on HBM-resident reads (no FASTQ parse, no PCIe)" % data_src)
+            workload = ("%s: %s x %d bp reads%s, k=%d, %s panel (%d patterns, %d keys), f_snp=%g, HBM-resident"
+                        % (args.config.upper(), "%gM" % (reads_total / 1e6) if strong_kernel else
+                           "%dM" % (R // 1_000_000), L, " in total over the GPUs" if strong_kernel else " per GPU",
+                           args.k, args.panel, n_pat, tinfo["n_keys"], args.f_snp))
+            scaling = "strong" if strong_kernel else "weak"
+            parallelism = "dp%d (reads sharded per rank, RCCL all-reduce of uint32 counts + u64 tally)" % world
         line = {
             "metric": "Mbases/sec (+ k-mers/sec) on %d bp FASTQ, k=%d" % (L, args.k),
-            "value": round(value, 1),
-            "unit": "Mbases/sec",
+            "value": value,
+            "unit": unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "strong" if strong else "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (counter-based generator, seed 42; patterns from %s, flanks seed 12345), "
-                    "resident in HBM: value is kernel-side throughput (no FASTQ parse, no PCIe); the "
-                    "reference's end-to-end metric is the e2e object" % (
-                        "SNP_GRCh38_hg38_wChr.bed" if args.panel == "grch38" else "a 200k-row synthetic BED"),
-            "config": {
-                "workload": "%s: %s x %d bp reads%s, k=%d, %s panel (%d patterns, %d keys), f_snp=%g"
-                            % (args.config.upper(), "%gM" % (reads_total / 1e6) if strong else "%dM" % (R // 1_000_000),
-                               L, " in total over the GPUs" if strong else " per GPU", args.k, args.panel, n_pat,
-                               tinfo["n_keys"], args.f_snp),
-                "reads_per_gpu": R, "reads_total": reads_total, "read_len": L, "k": args.k, "patterns": n_pat,
-                "filter_bytes": tinfo["filter_bytes"], "table_slots": tinfo["slots"],
-                "parallelism": "dp%d (reads sharded per rank, RCCL all-reduce of uint32 counts + u64 tally)" % world,
-            },
+            "data": data,
+            "config": {"workload": workload, "reads_per_gpu": R, "reads_total": reads_total, "read_len": L,
+                       "k": args.k, "patterns": n_pat, "filter_bytes": tinfo["filter_bytes"],
+                       "table_slots": tinfo["slots"], "parallelism": parallelism},
             "kmers_per_sec": round(kmer_rate, 1),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "kernel": "vc_count_reads_kernel (+ vc_count_long_kernel, empty here)",
-                "limiter": (LIMITER_LARGE_PANEL if tinfo["n_keys"] > 65536 else LIMITER_FLANK),
-                "kernel_ms": round(k_ms, 4),
-                "alg_bytes_per_launch": alg_bytes,
-                "alg_bytes_rule": "SURVEY.md 8(d): 1 B/base + 8 B/read",
-                "layout_bytes_per_launch": layout_bytes,
-                "frac_layout": round(layout_bytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            },
+            "roofline": kernel_obj,
             "cpu_baseline": cpu,
+            "vs_cpu_baseline": round(value / cpu["value"], 1) if cpu and headline else None,
             "parity_vs_reference_on_sample": parity,
             "parity_note": ("the product's .vaf on the first %d reads == the reference's (md5)" % n if world == 1 else
                             "all %d ranks count the first %d reads of the stream, %s all-reduce; == %d x the "
                             "reference's counts on that sample (u32)"
-                            % (world, n, "RCCL" if os.environ.get("VAFC_DIST_BACKEND", "nccl") == "nccl" else
-                               os.environ.get("VAFC_DIST_BACKEND"), world)),
+                            % (world, n, "RCCL" if backend == "nccl" else backend, world)),
+            "parity_full_size": full_parity,
             "build_id": vafc.tree_build_id(),
             "e2e": e2e,
+            "cli": cli,
         }
         print(json.dumps(line), flush=True)
     kmap.close()
-    import shutil
     shutil.rmtree(tmp, ignore_errors=True)
     if world > 1:
         dist.destroy_process_group()

@@ -203,6 +203,48 @@ typedef struct {
 int vc_count_file(vc_ctx *ctx, const char *path, int block_bases, int n_threads,
                   vc_file_stats *st);
 
+/* One rank's share of a file (one process per GPU, kmer-cnt_amd/vafc_dist.py):
+ * the records of a plain FASTA/FASTQ file whose header lies in the byte range
+ * [first, end), where first is the first record header at or after `begin`
+ * (begin = 0: the file's start; later: the record shape found there, as the
+ * parallel reader's pieces do, vafc_ingest.h).  Counted like vc_count_file,
+ * the block loop starting afresh at `first`.  The reference counts a file in
+ * one kseq stream (vaf-counter.c:486-517,550-582); consecutive ranges
+ * [b_0 = 0, b_1), [b_1, b_2), ... count exactly its reads iff every range's
+ * ri.first equals the previous range's ri.next and no range has ri.errs > 0
+ * (a -2 from the reader ends a block, and the reference's third-empty-block
+ * stop depends on the blocks before it).  The caller checks that and
+ * otherwise counts the file whole in one range (begin = 0, end = UINT64_MAX,
+ * which is vc_count_file's result).  gzip files (and anything but a regular
+ * file) are not split: begin = 0 counts the whole file (ri.whole = 1),
+ * begin > 0 counts nothing (ri.first = ri.next = UINT64_MAX, ri.whole = 1).
+ * VC_EIO if the file cannot be opened. */
+typedef struct {
+	uint64_t first;     /* header offset counting began at; UINT64_MAX: none found, nothing counted */
+	uint64_t next;      /* header offset of the first record at or past end; UINT64_MAX: the file ended */
+	uint64_t errs;      /* reader -2 returns (truncated records) met in the range */
+	uint32_t stopped;   /* the block loop ended the file inside the range */
+	uint32_t whole;     /* 1: the file is not split by ranges (gzip, pipe) */
+} vc_range_info;
+int vc_count_file_range(vc_ctx *ctx, const char *path, uint64_t begin, uint64_t end, int block_bases,
+                        int n_threads, vc_file_stats *st, vc_range_info *ri);
+/* Host-only: the same range through the parallel reader without a device;
+ * accepted read bytes / lengths copied out while they fit (as
+ * vc_scan_file_parallel). */
+int vc_scan_file_range(const char *path, int k, int block_bases, int n_threads, uint64_t piece_bytes,
+                       uint64_t begin, uint64_t end, vc_file_stats *st, vc_range_info *ri, uint8_t *seq_out,
+                       size_t seq_cap, uint32_t *lens_out, size_t lens_cap);
+
+/* Where the calling thread's last pass through the parallel reader
+ * (vc_count_file / vc_count_file_range on a plain or gzip file,
+ * vc_scan_file_parallel, vc_scan_file_range) spent its time: prof[0..7) =
+ * the reader's wall seconds; main-thread seconds waiting for the next piece,
+ * submitting pieces (H2D copies and kernel launches), re-parsing mis-guessed
+ * pieces; worker thread-seconds parsing, waiting for a slot the main thread
+ * had not released, waiting for a slot's previous copy to leave it.  Returns
+ * the pieces of that pass (0: none yet).  prof may be NULL. */
+uint64_t vc_ingest_profile(double *prof);
+
 /* Optional: allocate vc_count_file's parallel-reader buffers for n_threads
  * reader threads now (pinned host + device memory, about 20 MB per thread),
  * so that a later vc_count_file does not pay for the allocation.  Without

@@ -125,6 +125,26 @@ VC_HD uint32_t vc_l2f_mask(uint32_t h2)
 	return (1u << (h2 & 31u)) | (1u << ((h2 >> 5) & 31u)) | (1u << ((h2 >> 10) & 31u));
 }
 
+/* The same filter keyed by the two strands' low 32 bits instead of the
+ * canonical k-mer (build option VC_BIG_SYMQ, large-panel kernels only): the
+ * queue then holds (rlo << 32) | flo, which the drain tests with two
+ * multiplies and no reverse complement; only survivors rebuild the canonical
+ * k-mer (vc_canon_from_strands).  Symmetric in (flo, rlo), so it is a
+ * function of the canonical k-mer.  Word from the top bits of one mix, bits
+ * from a second one. */
+VC_HD uint32_t vc_l2s_hash(uint32_t flo, uint32_t rlo)
+{
+	uint32_t x = flo * 0x9E3779B1u + rlo * 0x9E3779B1u;
+	x ^= x >> 15;
+	return x * 0x85EBCA77u;
+}
+VC_HD uint32_t vc_l2s_hash2(uint32_t flo, uint32_t rlo)
+{
+	uint32_t y = (flo * 0x9E3779B1u) ^ (rlo * 0x9E3779B1u);
+	y ^= y >> 13;
+	return y * 0xC2B2AE3Du;
+}
+
 /* Large panels (a second-level filter in use) and k >= 21: a larger LDS
  * Bloom filter, VC_BIG_FILTER_WORDS 32-bit words (144 KiB: the queues shrink
  * to VC_BIG_QCAP entries per wave to make room), not a power of two.  Word

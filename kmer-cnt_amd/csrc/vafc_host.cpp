@@ -400,6 +400,16 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 			fw.swap(fbig);
 			c->big = 1;
 			c->qcap = VC_BIG_QCAP;
+#ifdef VC_BIG_SYMQ
+			// the big kernels queue both strands' low words: key the second
+			// level by them (vc_l2s_*) instead of the canonical k-mer
+			std::fill(l2w.begin(), l2w.end(), 0u);
+			for (const vc_slot_t &e : tab)
+				if (e.key != VC_EMPTY_KEY) {
+					const uint32_t flo = (uint32_t)e.key, rlo = (uint32_t)vc_revcomp(e.key, k);
+					l2w[vc_l2s_hash(flo, rlo) >> (32 - l2bits)] |= vc_l2f_mask(vc_l2s_hash2(flo, rlo));
+				}
+#endif
 		}
 		if (k >= VC_FLANK_MIN_K && !l2bits && !force_bloom) {
 			std::vector<uint32_t> fb((size_t)1 << VC_FLANK_WBITS, 0);
@@ -579,8 +589,18 @@ static int kc_launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const ui
 	return VC_OK;
 }
 
+// Whether any of n host-side read lengths takes the long-read kernel.
+static bool any_long(const uint32_t *lens, uint64_t n)
+{
+	uint32_t m = 0;
+	for (uint64_t i = 0; i < n; ++i) m = lens[i] > m ? lens[i] : m;
+	return m > VC_LONG_READ;
+}
+
+// may_long = false: the caller knows no read is longer than VC_LONG_READ (a
+// host batch), so the long-read kernel and its list reset are not launched.
 static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint64_t *d_offs,
-                  const uint32_t *d_lens, uint64_t n_reads, hipStream_t st)
+                  const uint32_t *d_lens, uint64_t n_reads, hipStream_t st, bool may_long = true)
 {
 	if (n_reads == 0) return VC_OK;
 	if (c->kc) return kc_launch(c, d_seq, seq_bytes, d_offs, d_lens, n_reads, st);
@@ -627,9 +647,9 @@ static int launch(vc_ctx *c, const uint8_t *d_seq, size_t seq_bytes, const uint6
 	A.flags = c->d_flags;
 	uint64_t groups = (n_reads + VC_BLOCK - 1) / VC_BLOCK;
 	int grid = (int)(groups < (uint64_t)c->n_cu ? groups : (uint64_t)c->n_cu);
-	HIPCK(hipMemsetAsync(c->d_nlong, 0, sizeof(uint32_t), st));
+	if (may_long) HIPCK(hipMemsetAsync(c->d_nlong, 0, sizeof(uint32_t), st));
 	if (c->timing) HIPCK(hipEventRecord(c->t0, st));
-	HIPCK(vc_launch_count(&A, grid, c->n_cu, st));
+	HIPCK(vc_launch_count(&A, grid, may_long ? c->n_cu : 0, st));
 	if (tiny) HIPCK(hipStreamSynchronize(st));   // d_pad is reused by the next tiny call
 	if (c->timing) {
 		HIPCK(hipEventRecord(c->t1, st));
@@ -722,7 +742,7 @@ static int slot_submit(vc_ctx *c, Slot &s, size_t bytes, uint64_t n_reads)
 		HIPCK(hipMemcpyAsync(s.d_seq, s.h_seq, bytes, hipMemcpyHostToDevice, c->st));
 		HIPCK(hipMemcpyAsync(s.d_offs, s.h_offs, n_reads * sizeof(uint64_t), hipMemcpyHostToDevice, c->st));
 		HIPCK(hipMemcpyAsync(s.d_lens, s.h_lens, n_reads * sizeof(uint32_t), hipMemcpyHostToDevice, c->st));
-		int rc = launch(c, s.d_seq, bytes, s.d_offs, s.d_lens, n_reads, c->st);
+		int rc = launch(c, s.d_seq, bytes, s.d_offs, s.d_lens, n_reads, c->st, any_long(s.h_lens, n_reads));
 		if (rc != VC_OK) return rc;
 		HIPCK(hipEventRecord(s.done, c->st));
 		s.pending = true;
@@ -1204,7 +1224,7 @@ public:
 		HIPCK(hipMemcpyAsync(s.d_seq, s.h_seq, bytes, hipMemcpyHostToDevice, sh->st));
 		HIPCK(hipMemcpyAsync(s.d_offs, s.h_offs, n * sizeof(uint64_t), hipMemcpyHostToDevice, sh->st));
 		HIPCK(hipMemcpyAsync(s.d_lens, s.h_lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, sh->st));
-		int rc = launch(sh, s.d_seq, bytes, s.d_offs, s.d_lens, n, sh->st);
+		int rc = launch(sh, s.d_seq, bytes, s.d_offs, s.d_lens, n, sh->st, any_long(s.h_lens, n));
 		if (rc != VC_OK) return rc;
 		HIPCK(hipEventRecord(s.done, sh->st));
 		s.pending = true;
@@ -1299,7 +1319,7 @@ extern "C" int vc_reserve_file_ingest(vc_ctx *c, int n_threads)
 }
 
 static int count_file_parallel(vc_ctx *c, int fd, uint64_t size, int block_bases, int n_threads,
-                               vc_file_stats &st)
+                               vc_file_stats &st, VcTextRange *range = nullptr)
 {
 	const int threads = clamp_threads(n_threads);
 	const int slots = reserve_ingest(c, threads, false);
@@ -1307,7 +1327,7 @@ static int count_file_parallel(vc_ctx *c, int fd, uint64_t size, int block_bases
 	DeviceSink sink(c);
 	const char *pe = getenv("VAFC_INGEST_PIECE");          // test knob: piece size in bytes
 	const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : VC_PIECE_BYTES;
-	return vc_ingest_plain(fd, size, c->k, block_bases, threads, slots, piece, sink, st);
+	return vc_ingest_plain(fd, size, c->k, block_bases, threads, slots, piece, sink, st, range);
 }
 
 // gzip input: the text the parallel inflater produces (n_threads workers) is
@@ -1441,6 +1461,45 @@ extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n
 	                    [&bw](const char *s, size_t l) { return bw.add(s, l); }, local);
 	if (rc == VC_OK) rc = bw.flush();
 	if (rc == VC_OK) rc = sync_shards(c);
+	local.seconds = wall_now() - t0;
+	if (st) *st = local;
+	return rc;
+}
+
+extern "C" int vc_count_file_range(vc_ctx *c, const char *path, uint64_t begin, uint64_t end, int block_bases,
+                                   int n_threads, vc_file_stats *st, vc_range_info *ri)
+{
+	if (!c || !path || !ri || end <= begin) return VC_EINVAL;
+	vc_file_stats local = {0, 0, 0, 0.0};
+	*ri = vc_range_info{UINT64_MAX, UINT64_MAX, 0, 0, 1};
+	const double t0 = wall_now();
+	const int fd = open(path, O_RDONLY);
+	if (fd < 0) return VC_EIO;
+	struct stat sb;
+	uint8_t magic[2] = {0, 0};
+	const bool reg = fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
+	const bool gz = reg && pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+	if (!reg || gz) {   // not split: the first range counts the whole file
+		close(fd);
+		if (begin > 0) {
+			if (st) *st = local;
+			return VC_OK;
+		}
+		const int rc = vc_count_file(c, path, block_bases, n_threads, st);
+		if (rc == VC_OK) *ri = vc_range_info{0, UINT64_MAX, 0, 1, 1};
+		return rc;
+	}
+	int rc = hipSetDevice(c->dev) == hipSuccess ? VC_OK : VC_EHIP;
+	VcTextRange R;
+	R.begin = begin;
+	R.end = end;
+	if (rc == VC_OK) {
+		VcAffinityScope placement(gpu_cpus(c, clamp_threads(n_threads)));
+		rc = count_file_parallel(c, fd, (uint64_t)sb.st_size, block_bases, n_threads, local, &R);
+	}
+	close(fd);
+	if (rc == VC_OK) rc = sync_shards(c);
+	*ri = vc_range_info{R.first, R.next, R.errs, R.stopped ? 1u : 0u, 0u};
 	local.seconds = wall_now() - t0;
 	if (st) *st = local;
 	return rc;

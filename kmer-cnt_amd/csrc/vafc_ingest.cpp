@@ -394,6 +394,8 @@ uint64_t replay_blocks(const Piece &P, int block_bases, BlockState &S, vc_file_s
 
 } // namespace
 
+thread_local VcIngestProfile vc_ingest_last;
+
 static double ing_now()
 {
 	struct timespec ts;
@@ -402,20 +404,39 @@ static double ing_now()
 }
 
 int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int slots, uint64_t piece_bytes,
-                   VcIngestSink &sink, vc_file_stats &st)
+                   VcIngestSink &sink, vc_file_stats &st, VcTextRange *range)
 {
-	const bool prof = getenv("VAFC_INGEST_PROFILE") != nullptr;
+	// timings are always taken (a few clock reads per piece of megabytes);
+	// VAFC_INGEST_PROFILE also prints them
+	const bool prof_print = getenv("VAFC_INGEST_PROFILE") != nullptr;
+	vc_ingest_last = VcIngestProfile();
 	double t_wait = 0, t_submit = 0, t_reparse = 0;
-	std::atomic<uint64_t> t_parse_us{0}, t_slotwait_us{0};
+	std::atomic<uint64_t> t_parse_us{0}, t_slotwait_us{0}, t_acquire_us{0};
 	const double t_begin = ing_now();
 	if (threads < 1 || slots < threads + 1 || piece_bytes < 2) return VC_EINVAL;
+	// the range [r0, r1) of the text (the whole text without one)
+	const uint64_t r0 = range ? range->begin : 0, r1 = range ? range->end : UINT64_MAX;
+	if (range) {
+		if (r1 <= r0) return VC_EINVAL;
+		range->first = r0 == 0 ? 0 : UINT64_MAX;
+		range->next = UINT64_MAX;
+		range->errs = 0;
+		range->stopped = false;
+	}
+	if (!src.longer_than(r0)) {   // empty input / range past the end: nothing counted
+		if (range) range->first = UINT64_MAX;
+		return VC_OK;
+	}
 	if (!src.longer_than(0)) return VC_OK;   // empty input: three empty blocks, nothing counted
 	bool fasta = false;
 	{
 		VcFastqReader rd;
 		if (!rd.open_src(&src, 0, (size_t)1 << 16)) return VC_ENOMEM;
 		const int64_t h = rd.peek_header();
-		if (h < 0) return VC_OK;      // no record at all
+		if (h < 0) {                  // no record at all
+			if (range) range->first = UINT64_MAX;
+			return VC_OK;
+		}
 		uint8_t c = 0;
 		if (src.read(&c, 1, (uint64_t)h) == 1) fasta = c == '>';
 	}
@@ -436,31 +457,34 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 		std::vector<uint8_t> tmp;
 		for (;;) {
 			const uint64_t j = next.fetch_add(1);
-			const double w0 = prof ? ing_now() : 0;
+			const double w0 = ing_now();
 			{
 				std::unique_lock<std::mutex> lk(mu);
 				cv.wait(lk, [&] { return abort || released + (uint64_t)slots > j; });
 				if (abort || j >= n_pieces) return;
 			}
-			if (!src.longer_than(j * piece_bytes)) {
+			// piece j of the range: [r0 + j P, min(r0 + (j + 1) P, r1))
+			const uint64_t pa = r0 + j * piece_bytes;
+			if (pa >= r1 || !src.longer_than(pa)) {
 				std::lock_guard<std::mutex> lk(mu);
 				if (j < n_pieces) n_pieces = j;
 				cv.notify_all();
 				return;
 			}
-			const double w1 = prof ? ing_now() : 0;
+			const double w1 = ing_now();
 			const int slot = (int)(j % (uint64_t)slots);
 			Piece &P = pcs[(size_t)slot];
 			P.j = j;
-			P.a = j * piece_bytes;
-			P.b = P.a + piece_bytes;
+			P.a = pa;
+			P.b = r1 - pa > piece_bytes ? pa + piece_bytes : r1;
 			int rc = sink.acquire(slot, &P.buf);
+			t_acquire_us += (uint64_t)((ing_now() - w1) * 1e6);
 			if (rc == VC_OK) {
-				const int64_t g = j == 0 ? 0 : guess_record(src, P.a, fasta, tmp);
+				const int64_t g = P.a == 0 ? 0 : guess_record(src, P.a, fasta, tmp);
 				if (g >= 0) rc = parse_piece(src, (uint64_t)g, k, slot, sink, rd, P);
 				else P.start = -1;
 			}
-			if (prof) {
+			{
 				const double w2 = ing_now();
 				t_slotwait_us += (uint64_t)((w1 - w0) * 1e6);
 				t_parse_us += (uint64_t)((w2 - w1) * 1e6);
@@ -482,35 +506,52 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 	for (uint64_t j = 0;; ++j) {
 		const int slot = (int)(j % (uint64_t)slots);
 		Piece &P = pcs[(size_t)slot];
-		const double m0 = prof ? ing_now() : 0;
+		const double m0 = ing_now();
 		{
 			std::unique_lock<std::mutex> lk(mu);
 			cv.wait(lk, [&] { return (P.ready && P.j == j) || n_pieces <= j; });
 			if (!(P.ready && P.j == j)) break;   // past the end of the text
 		}
 		np = j + 1;
-		if (prof) t_wait += ing_now() - m0;
+		t_wait += ing_now() - m0;
 		if (rc == VC_OK) rc = P.rc;
+		if (j == 0 && r0 > 0) {
+			// a range's first header is its first piece's guess; none found:
+			// nothing is counted (the previous range's `next` tells whether
+			// that is right)
+			if (P.start < 0) {
+				src.release(P.a);
+				std::lock_guard<std::mutex> lk(mu);
+				P.ready = false;
+				released = 1;
+				abort = true;
+				cv.notify_all();
+				break;
+			}
+			expect = (uint64_t)P.start;
+			if (range) range->first = expect;
+		}
 		if (rc == VC_OK && !S.stopped && P.b > expect) {
 			if (P.start < 0 || (uint64_t)P.start != expect) { // a wrong guess: parse from the true boundary
-				const double r0 = prof ? ing_now() : 0;
+				const double r0 = ing_now();
 				rc = parse_piece(src, expect, k, slot, sink, rd, P);
-				if (prof) t_reparse += ing_now() - r0;
+				t_reparse += ing_now() - r0;
 			}
 			if (rc == VC_OK) {
 				expect = P.end;
+				if (range) range->errs += P.errs.size();
 				const uint64_t keep = replay_blocks(P, block_bases, S, st);
 				if (keep) {
 					const uint64_t bytes = (uint64_t)P.buf.offs[keep - 1] + P.buf.lens[keep - 1];
-					const double s0 = prof ? ing_now() : 0;
+					const double s0 = ing_now();
 					rc = sink.submit(slot, P.buf, keep, bytes);
-					if (prof) t_submit += ing_now() - s0;
+					t_submit += ing_now() - s0;
 				}
 			}
 		}
 		// later reads start at the next piece's guess (one byte before it) or
 		// at the next record boundary
-		const uint64_t nxt = (j + 1) * piece_bytes - 1;
+		const uint64_t nxt = r0 + (j + 1) * piece_bytes - 1;
 		src.release(expect < nxt ? expect : nxt);
 		const bool done = rc != VC_OK || S.stopped;
 		{
@@ -524,11 +565,29 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 	}
 	src.abort();   // wake workers still reading pieces that are no longer needed
 	for (auto &t : pool) t.join();
-	if (prof)
+	{
+		VcIngestProfile &L = vc_ingest_last;
+		L.total = ing_now() - t_begin;
+		L.main_wait = t_wait;
+		L.submit = t_submit;
+		L.reparse = t_reparse;
+		L.parse = (t_parse_us.load() - t_acquire_us.load()) * 1e-6;
+		L.slot_wait = t_slotwait_us.load() * 1e-6;
+		L.acquire = t_acquire_us.load() * 1e-6;
+		L.pieces = np;
+		L.threads = threads;
+	}
+	if (prof_print)
 		fprintf(stderr, "[ingest] %llu pieces, %d threads: total %.3f s; main: wait %.3f submit %.3f reparse %.3f; "
-		        "workers: parse %.3f slot-wait %.3f (thread-seconds)\n", (unsigned long long)np, threads,
-		        ing_now() - t_begin, t_wait, t_submit, t_reparse, t_parse_us.load() * 1e-6,
-		        t_slotwait_us.load() * 1e-6);
+		        "workers: parse %.3f slot-wait %.3f acquire %.3f (thread-seconds)\n", (unsigned long long)np, threads,
+		        vc_ingest_last.total, t_wait, t_submit, t_reparse, vc_ingest_last.parse, vc_ingest_last.slot_wait,
+		        vc_ingest_last.acquire);
+	if (range) {
+		range->stopped = S.stopped;
+		range->next = S.stopped ? UINT64_MAX : expect;
+		if (range->first == UINT64_MAX) range->next = UINT64_MAX;
+		return rc;
+	}
 	if (rc == VC_OK && !S.stopped) {
 		// the text ended inside a record the last piece never reached (cannot
 		// happen: the last piece parses to the end of the text) -- be explicit
@@ -538,10 +597,10 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 }
 
 int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, int slots,
-                    uint64_t piece_bytes, VcIngestSink &sink, vc_file_stats &st)
+                    uint64_t piece_bytes, VcIngestSink &sink, vc_file_stats &st, VcTextRange *range)
 {
 	FdSource src(fd, size);
-	return vc_ingest_text(src, k, block_bases, threads, slots, piece_bytes, sink, st);
+	return vc_ingest_text(src, k, block_bases, threads, slots, piece_bytes, sink, st, range);
 }
 
 int vc_ingest_gzip(VcGzParallel *g, int k, int block_bases, int threads, int slots, uint64_t piece_bytes,
@@ -687,4 +746,58 @@ extern "C" int vc_scan_file_parallel(const char *path, int k, int block_bases, i
 	local.seconds = mono_now() - t0;
 	*st = local;
 	return rc;
+}
+
+extern "C" int vc_scan_file_range(const char *path, int k, int block_bases, int n_threads, uint64_t piece_bytes,
+                                  uint64_t begin, uint64_t end, vc_file_stats *st, vc_range_info *ri,
+                                  uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out, size_t lens_cap)
+{
+	if (!path || !st || !ri || n_threads < 1 || piece_bytes < 2 || end <= begin) return VC_EINVAL;
+	vc_file_stats local = {0, 0, 0, 0.0};
+	*ri = vc_range_info{UINT64_MAX, UINT64_MAX, 0, 0, 1};
+	const double t0 = mono_now();
+	const int fd = open(path, O_RDONLY);
+	if (fd < 0) return VC_EIO;
+	struct stat sb;
+	uint8_t magic[2] = {0, 0};
+	const bool reg = fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
+	if (!reg || (pread_full(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b)) {
+		close(fd);   // not split (vc_count_file_range): the first range takes the whole file
+		int rc = VC_OK;
+		if (begin == 0) {
+			rc = vc_scan_file_parallel(path, k, block_bases, n_threads, piece_bytes, &local, seq_out, seq_cap,
+			                           lens_out, lens_cap);
+			if (rc == VC_OK) *ri = vc_range_info{0, UINT64_MAX, 0, 1, 1};
+		}
+		local.seconds = mono_now() - t0;
+		*st = local;
+		return rc;
+	}
+	const int slots = n_threads < 2 ? n_threads + 2 : 2 * n_threads;
+	HostSink sink(slots, piece_bytes, seq_out, seq_cap, lens_out, lens_cap);
+	VcTextRange R;
+	R.begin = begin;
+	R.end = end;
+	const int rc = vc_ingest_plain(fd, (uint64_t)sb.st_size, k, block_bases, n_threads, slots, piece_bytes, sink,
+	                               local, &R);
+	close(fd);
+	*ri = vc_range_info{R.first, R.next, R.errs, R.stopped ? 1u : 0u, 0u};
+	local.seconds = mono_now() - t0;
+	*st = local;
+	return rc;
+}
+
+extern "C" uint64_t vc_ingest_profile(double *prof)
+{
+	const VcIngestProfile &L = vc_ingest_last;
+	if (prof) {
+		prof[0] = L.total;
+		prof[1] = L.main_wait;
+		prof[2] = L.submit;
+		prof[3] = L.reparse;
+		prof[4] = L.parse;
+		prof[5] = L.slot_wait;
+		prof[6] = L.acquire;
+	}
+	return L.pieces;
 }

@@ -95,15 +95,46 @@ public:
 	virtual void abort() {}
 };
 
-// Whole-text pass.  threads >= 1 parse workers, `slots` >= threads + 1 slot
-// buffers owned by the sink (piece j uses slot j % slots), pieces of
-// `piece_bytes`.  Fills st (bases, seqs, blocks; not seconds).
-int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int slots, uint64_t piece_bytes,
-                   VcIngestSink &sink, vc_file_stats &st);
+// A byte range of the text (one rank's share of a file, vc_count_file_range):
+// the records whose header lies in [first, end), where first is the header
+// found at or after begin (begin = 0: the text's start; later: a guess, as for
+// a piece, that only the previous range's `next` can confirm).  The block
+// loop starts afresh at `first`.  Out: first (UINT64_MAX: no header found
+// within the reader's look-ahead -- nothing was counted), next (the header of
+// the first record at or past end; UINT64_MAX: the text ended first), errs
+// (reader -2 returns met) and stopped (the block loop ended the text inside
+// the range).  Consecutive ranges count exactly the whole text's reads iff each
+// range's first equals the previous range's next and no range met a -2
+// (without one, a block ends empty only at the end of the text).
+struct VcTextRange {
+	uint64_t begin = 0, end = UINT64_MAX;
+	uint64_t first = 0, next = UINT64_MAX, errs = 0;
+	bool stopped = false;
+};
 
-// An open plain file of `size` bytes.
+// Where the last vc_ingest_text pass of the calling thread spent its time
+// (vc_ingest_profile, include/vafc.h): wall seconds, main-thread seconds
+// waiting for the next piece, submitting pieces (the sink: H2D copies and
+// kernel launches), re-parsing mis-guessed pieces; worker thread-seconds
+// parsing, waiting for a slot the main thread has not released, and waiting
+// in the sink's acquire (the slot's previous copy still in flight).
+struct VcIngestProfile {
+	double total = 0, main_wait = 0, submit = 0, reparse = 0, parse = 0, slot_wait = 0, acquire = 0;
+	uint64_t pieces = 0;
+	int threads = 0;
+};
+extern thread_local VcIngestProfile vc_ingest_last;
+
+// Whole-text pass (range == NULL) or the records of one range.  threads >= 1
+// parse workers, `slots` >= threads + 1 slot buffers owned by the sink (piece j
+// uses slot j % slots), pieces of `piece_bytes`.  Fills st (bases, seqs,
+// blocks; not seconds).
+int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int slots, uint64_t piece_bytes,
+                   VcIngestSink &sink, vc_file_stats &st, VcTextRange *range = nullptr);
+
+// An open plain file of `size` bytes (the whole text, or one range of it).
 int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, int slots,
-                    uint64_t piece_bytes, VcIngestSink &sink, vc_file_stats &st);
+                    uint64_t piece_bytes, VcIngestSink &sink, vc_file_stats &st, VcTextRange *range = nullptr);
 
 // A gzip file opened with vc_gzp_open (vafc_gzip.h; the caller closes it): a
 // pump thread copies the inflated stream into a window of blocks that the

@@ -229,6 +229,15 @@ __device__ __forceinline__ uint64_t revcomp_dev(uint64_t x, int k)
 	return (~r) >> (64 - 2 * k);
 }
 
+// Ablation bits of the drain (VC_ABLATION builds only, with ABL 1/2/4 above;
+// results are wrong by design): 1024 = queued entries are dropped, never
+// drained; 2048 = the drain computes every entry's second-level word and
+// mask but issues no gather and probes nothing; 4096 = the second-level
+// gather runs, survivors are not probed in the exact table.
+#define VC_ABL_NODRAIN 1024
+#define VC_ABL_NOGATHER 2048
+#define VC_ABL_NOPROBE 4096
+
 // key: the raw forward k-mer (bits above 2k may hold older bases).
 __device__ __forceinline__ void probe_and_count(const VcKernelArgs &A, uint64_t fwd_raw)
 {
@@ -258,6 +267,27 @@ struct WaveQueue {
 // memory latency covers the whole drain.
 // Large key sets: every entry is first checked against the second-level
 // filter (one L2-resident dword), and only survivors probe the exact table.
+template <int ABL>
+__device__ __forceinline__ void probe_key(const VcKernelArgs &A, uint64_t key, uint32_t h)
+{
+	if constexpr ((ABL & VC_ABL_NOPROBE) != 0) {
+		asm volatile("" :: "v"(h), "v"(key));
+		return;
+	}
+	uint32_t t = vc_table_slot(h, A.tbits);
+	for (;;) {
+		const uint4 e = *reinterpret_cast<const uint4 *>(&A.table[t]);
+		const uint64_t k2 = ((uint64_t)e.y << 32) | e.x;
+		if (k2 == key) {
+			atomicAdd(&A.counts[e.z], 1u);
+			break;
+		}
+		if (k2 == VC_EMPTY_KEY) break;
+		t = (t + 1u) & A.tmask;
+	}
+}
+
+template <int ABL>
 __device__ __forceinline__ void drain_range_l2f(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
                                              uint32_t hi, int lane)
 {
@@ -277,32 +307,89 @@ __device__ __forceinline__ void drain_range_l2f(const VcKernelArgs &A, const uin
 			key[r] = f < rc ? f : rc;
 			h[r] = vc_hash(key[r]);
 			m[r] = vc_l2f_mask(vc_hash2(key[r]));
-			w[r] = A.l2f[h[r] >> l2sh];
+			if constexpr ((ABL & VC_ABL_NOGATHER) != 0) asm volatile("" :: "v"(h[r] >> l2sh), "v"(m[r]));
+			else w[r] = A.l2f[h[r] >> l2sh];
 		}
 	}
+	if constexpr ((ABL & VC_ABL_NOGATHER) != 0) return;
 #pragma unroll
 	for (int r = 0; r < 4; ++r) {
 		if ((w[r] & m[r]) != m[r]) continue;      // also skips empty entries (w = 0, m = 1)
-		uint32_t t = vc_table_slot(h[r], A.tbits);
-		for (;;) {
-			const uint4 e = *reinterpret_cast<const uint4 *>(&A.table[t]);
-			const uint64_t k2 = ((uint64_t)e.y << 32) | e.x;
-			if (k2 == key[r]) {
-				atomicAdd(&A.counts[e.z], 1u);
-				break;
-			}
-			if (k2 == VC_EMPTY_KEY) break;
-			t = (t + 1u) & A.tmask;
-		}
+		probe_key<ABL>(A, key[r], h[r]);
 	}
 }
 
+// Canonical k-mer of a window from its two strands' low 32 bits (K >= 16:
+// the first sixteen bases, complemented, are rlo; the last sixteen are flo):
+// forward = rc16(rlo) << 2(K - 16) | flo, reverse = rc16(flo) << 2(K - 16) | rlo.
+__device__ __forceinline__ uint32_t rc16(uint32_t x)
+{
+	x = __builtin_bitreverse32(x);
+	return ~(((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1));
+}
+__device__ __forceinline__ uint64_t vc_canon_from_strands(uint32_t flo, uint32_t rlo, int k)
+{
+	const uint32_t sh = 2u * (uint32_t)(k - 16);
+	const uint64_t f = ((uint64_t)rc16(rlo) << sh) | flo;
+	const uint64_t r = ((uint64_t)rc16(flo) << sh) | rlo;
+	return f < r ? f : r;
+}
+
+// Large-panel kernels with VC_BIG_SYMQ: entries are (rlo << 32) | flo and the
+// second-level filter is keyed by the strands (vc_l2s_*); only survivors
+// rebuild the canonical k-mer and hash it for the exact table.
+template <int ABL>
+__device__ __forceinline__ void drain_range_sym(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
+                                                uint32_t hi, int lane)
+{
+	uint32_t fl[4], rl[4], w[4], m[4];
+	const uint32_t l2sh = 32u - A.l2bits;
+#pragma unroll
+	for (int r = 0; r < 4; ++r) {
+		const uint32_t i = lo + (uint32_t)(r * WAVE + lane);
+		fl[r] = rl[r] = 0;
+		w[r] = 0;
+		m[r] = 1;
+		if (i < hi) {
+			const uint64_t e = q[i];
+			fl[r] = (uint32_t)e;
+			rl[r] = (uint32_t)(e >> 32);
+			const uint32_t hw = vc_l2s_hash(fl[r], rl[r]);
+			m[r] = vc_l2f_mask(vc_l2s_hash2(fl[r], rl[r]));
+			if constexpr ((ABL & VC_ABL_NOGATHER) != 0) asm volatile("" :: "v"(hw >> l2sh), "v"(m[r]));
+			else w[r] = A.l2f[hw >> l2sh];
+		}
+	}
+	if constexpr ((ABL & VC_ABL_NOGATHER) != 0) return;
+#pragma unroll
+	for (int r = 0; r < 4; ++r) {
+		if ((w[r] & m[r]) != m[r]) continue;      // also skips empty entries (w = 0, m = 1)
+		const uint64_t key = vc_canon_from_strands(fl[r], rl[r], A.k);
+		probe_key<ABL>(A, key, vc_hash(key));
+	}
+}
+
+#ifdef VC_BIG_SYMQ
+#define VC_SYMQ(ABL) (((ABL) & VC_KV_BIG) != 0)
+#else
+#define VC_SYMQ(ABL) false
+#endif
+
+template <int ABL>
 __device__ __forceinline__ void drain_range(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
                                             uint32_t hi, int lane)
 {
 	__builtin_amdgcn_wave_barrier();
+	if constexpr ((ABL & VC_ABL_NODRAIN) != 0) {
+		asm volatile("" :: "v"(q[lo + (uint32_t)lane]));
+		return;
+	}
+	if constexpr (VC_SYMQ(ABL)) {
+		drain_range_sym<ABL>(A, q, lo, hi, lane);
+		return;
+	}
 	if (A.l2bits) {
-		drain_range_l2f(A, q, lo, hi, lane);
+		drain_range_l2f<ABL>(A, q, lo, hi, lane);
 		return;
 	}
 	uint64_t key[4];
@@ -342,6 +429,7 @@ __device__ __forceinline__ void drain_range(const VcKernelArgs &A, const uint64_
 // Lanes with `hit` append `key` (bal = ballot(hit) != 0).  The queue is
 // normally drained once per read group (queue_flush); only a nearly full
 // queue is drained here, 64 entries from its top.
+template <int ABL>
 __device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q, uint64_t bal,
                                              bool hit, uint64_t key, int lane)
 {
@@ -350,7 +438,7 @@ __device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q
 	if (hit) Q.q[Q.n + pre] = key;
 	Q.n = __builtin_amdgcn_readfirstlane(Q.n + (uint32_t)__popcll(bal));
 	if (Q.n > A.qcap - WAVE) {        // A.qcap >= 2 WAVE
-		drain_range(A, Q.q, Q.n - WAVE, Q.n, lane);
+		drain_range<ABL>(A, Q.q, Q.n - WAVE, Q.n, lane);
 		Q.n -= WAVE;
 		// leave nothing in flight on this (rare) path, so that the compiler
 		// can keep counting the scan's prefetches across it
@@ -358,9 +446,10 @@ __device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q
 	}
 }
 
+template <int ABL>
 __device__ __forceinline__ void queue_flush(const VcKernelArgs &A, WaveQueue &Q, int lane)
 {
-	if (Q.n) drain_range(A, Q.q, 0, Q.n, lane);
+	if (Q.n) drain_range<ABL>(A, Q.q, 0, Q.n, lane);
 	Q.n = 0;
 }
 
@@ -517,7 +606,7 @@ __device__ __forceinline__ void scan_span(const VcKernelArgs &A, const uint32_t 
 				const bool hit = (fw[j] & fm[j]) == fm[j];
 				const uint64_t bal = __ballot(hit);
 				if constexpr ((ABL & 4) != 0) { asm volatile("" :: "s"(bal)); }
-				else if (bal) queue_append(A, Q, bal, hit, ((uint64_t)fh[j] << 32) | fl[j], lane);
+				else if (bal) queue_append<ABL>(A, Q, bal, hit, ((uint64_t)fh[j] << 32) | fl[j], lane);
 			}
 		}
 		w0 = w4; w1 = x1; w2 = x2; w3 = x3; w4 = x4;
@@ -877,8 +966,18 @@ __device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, i
 			// lowest pass first; lanes without one compute a garbage key they do not append
 			const uint32_t b = (uint32_t)__builtin_ctz(hm | 0x80000000u);   // hm < 2^16
 			const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, 2u * b);
-			const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
-			queue_append(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
+			if constexpr (VC_SYMQ(ABL)) {
+				// the reverse strand's low word: the C stream from the window's
+				// first base, s2 = 48 - K - b bases into chunk c - 2 (2 <= s2 <= 27
+				// for K >= 21); v_alignbit takes the shift modulo 32
+				const uint32_t s2 = (uint32_t)(48 - K) - b;
+				const bool up = s2 >= 16u;
+				const uint32_t rlo = __builtin_amdgcn_alignbit(up ? Cc : Cm1, up ? Cm1 : Cm2, 2u * s2);
+				queue_append<ABL>(A, Q, bal, has, ((uint64_t)rlo << 32) | flo, lane);
+			} else {
+				const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
+				queue_append<ABL>(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
+			}
 			hm &= hm - 1u;
 		}
 	}
@@ -899,6 +998,8 @@ __device__ __forceinline__ void hit_loop2(const VcKernelArgs &A, WaveQueue &Q, u
                                           uint32_t Bam1, uint32_t Ba, uint32_t Bb, int lane)
 {
 	constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
+	static_assert(!(VC_SYMQ(ABL) && VC_KV_BIG_DEFER != 0),
+	              "hit_loop2 queues forward k-mers (VC_DEFER_BIG and VC_BIG_SYMQ exclude each other)");
 	if constexpr ((ABL & 4) != 0) {
 		asm volatile("" :: "v"(hm));
 	} else if (__ballot(hm != 0u)) {
@@ -912,7 +1013,7 @@ __device__ __forceinline__ void hit_loop2(const VcKernelArgs &A, WaveQueue &Q, u
 			const uint32_t lo = ina ? Ba : Bb, hi = ina ? Bam1 : Ba, hi2 = ina ? Bam2 : Bam1;
 			const uint32_t flo = __builtin_amdgcn_alignbit(hi, lo, 2u * b);
 			const uint32_t fhi = __builtin_amdgcn_alignbit(hi2, hi, 2u * b) & HIM;
-			queue_append(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
+			queue_append<ABL>(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
 			hm &= hm - 1u;
 		}
 	}
@@ -1408,7 +1509,7 @@ __device__ __forceinline__ uint32_t packed_chunk_fb(const VcKernelArgs &A, const
 			const uint32_t b = (uint32_t)__builtin_ctz(hm | 0x80000000u);
 			const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, 2u * b);
 			const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
-			queue_append(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
+			queue_append<ABL>(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
 			hm &= hm - 1u;
 		}
 	}
@@ -1715,12 +1816,12 @@ vc_count_reads_kernel(VcKernelArgs A)
 		// drain at a group end only once the queue holds more than 112 entries
 		// (two per lane): each drain exposes one probe latency, so fewer, fuller
 		// drains cost less (C2: -1.6 %, C5: +-0; ABL 64 = a drain per group)
-		if constexpr ((ABL & 64) != 0) queue_flush(A, Q, lane);
-		else if ((int)Q.n > (int)A.qcap - 2 * WAVE) queue_flush(A, Q, lane);
+		if constexpr ((ABL & 64) != 0) queue_flush<ABL>(A, Q, lane);
+		else if ((int)Q.n > (int)A.qcap - 2 * WAVE) queue_flush<ABL>(A, Q, lane);
 		g = gn;
 		r = rn;
 	}
-	queue_flush(A, Q, lane);
+	queue_flush<ABL>(A, Q, lane);
 	const unsigned long long t = wave_sum_u64(tally);
 	if (lane == 0 && t) atomicAdd(A.tally, t);
 }
@@ -1774,7 +1875,7 @@ vc_count_long_kernel(VcKernelArgs A)
 			tally += tl;
 		}
 	}
-	queue_flush(A, Q, lane);
+	queue_flush<ABL>(A, Q, lane);
 	const unsigned long long t = wave_sum_u64(tally);
 	if (lane == 0 && t) atomicAdd(A.tally, t);
 }
@@ -1789,14 +1890,18 @@ static hipError_t launch_kw(const VcKernelArgs *A, int grid, int grid_long, hipS
 	const size_t lds = vc_lds_bytes(A->fwords, A->qcap);
 	hipLaunchKernelGGL((vc_count_reads_kernel<K, ABL>), dim3(grid), dim3(VC_BLOCK), lds, st, *A);
 	hipError_t e = hipGetLastError();
-	if (e != hipSuccess) return e;
+	if (e != hipSuccess || grid_long <= 0) return e;   // grid_long 0: the host knows there is no long read
 	hipLaunchKernelGGL((vc_count_long_kernel<K, ABL & (VC_KV_FLANK | VC_KV_BIG)>), dim3(grid_long), dim3(VC_BLOCK),
 	                   lds, st, *A);
 	return hipGetLastError();
 }
 
 #ifdef VC_ABLATION
-#define VC_ABL_LIST(X) X(1) X(2) X(4) X(3) X(5) X(6) X(7) X(8) X(12) X(16) X(20) X(64)
+#ifdef VC_ABL_SHORT   // the drain decomposition only (compiles in a fraction of the time)
+#define VC_ABL_LIST(X) X(1) X(2) X(4) X(7) X(1024) X(2048) X(4096)
+#else
+#define VC_ABL_LIST(X) X(1) X(2) X(4) X(3) X(5) X(6) X(7) X(8) X(12) X(16) X(20) X(64) X(1024) X(2048) X(4096)
+#endif
 #endif
 
 template <int K>
@@ -1808,6 +1913,7 @@ static hipError_t launch_k_impl(const VcKernelArgs *A, int grid, int grid_long, 
 #define VC_ABL_CASE(n)                                                                          \
 	case n:                                                                                     \
 		return A->flank ? launch_kw<21, n | VC_KV_FLANK>(A, grid, grid_long, st)                \
+		     : A->big   ? launch_kw<21, n | VC_KV_BIG>(A, grid, grid_long, st)                  \
 		                : launch_kw<21, n>(A, grid, grid_long, st);
 			VC_ABL_LIST(VC_ABL_CASE)
 #undef VC_ABL_CASE
@@ -1852,6 +1958,9 @@ static hipError_t setup_k_impl(int lds)
 		                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);               \
 	if (e == hipSuccess)                                                                        \
 		e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<21, n | VC_KV_FLANK>,       \
+		                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);               \
+	if (e == hipSuccess)                                                                        \
+		e = hipFuncSetAttribute((const void *)vc_count_reads_kernel<21, n | VC_KV_BIG>,         \
 		                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 		VC_ABL_LIST(VC_ABL_SET)
 #undef VC_ABL_SET

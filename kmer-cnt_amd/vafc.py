@@ -39,7 +39,9 @@ EXPORTS = (
     "vc_write_vaf", "vc_pattern_fields", "vc_free", "vc_create", "vc_destroy",
     "vc_count_block", "vc_count_device", "vc_finish", "vc_reset", "vc_device_counts",
     "vc_bind_outputs", "vc_device_tally", "vc_stream", "vc_set_timing", "vc_kernel_ms",
-    "vc_table_info", "vc_create_multi", "vc_shard_count", "vc_shard_info", "vc_count_file", "vc_scan_file", "vc_scan_file_parallel", "vc_scan_records", "vc_reserve_file_ingest",
+    "vc_table_info", "vc_create_multi", "vc_shard_count", "vc_shard_info", "vc_count_file",
+    "vc_count_file_range", "vc_scan_file_range", "vc_ingest_profile", "vc_scan_file", "vc_scan_file_parallel",
+    "vc_scan_records", "vc_reserve_file_ingest",
     "vc_gz_inflate_parallel", "vc_gz_inflate_zlib", "vc_gz_crc32",
     "vc_fasta_load", "vc_fasta_count", "vc_fasta_name", "vc_fasta_seq", "vc_fasta_data", "vc_fasta_free",
     "vc_count_candidates", "vc_set_nt4_decode",
@@ -64,6 +66,16 @@ class VafcError(RuntimeError):
 class FileStats(C.Structure):
     _fields_ = [("bases", C.c_uint64), ("seqs", C.c_uint64), ("blocks", C.c_uint64),
                 ("seconds", C.c_double)]
+
+
+class RangeInfo(C.Structure):
+    """vc_range_info: where one rank's byte range of a file began and ended
+    (include/vafc.h, vc_count_file_range)."""
+    _fields_ = [("first", C.c_uint64), ("next", C.c_uint64), ("errs", C.c_uint64),
+                ("stopped", C.c_uint32), ("whole", C.c_uint32)]
+
+
+NO_OFFSET = (1 << 64) - 1   # vc_range_info's UINT64_MAX
 
 
 _lib = None
@@ -116,6 +128,12 @@ def lib():
         "vc_table_info": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                     C.POINTER(C.c_uint64)]),
         "vc_count_file": (C.c_int, [P, C.c_char_p, C.c_int, C.c_int, C.POINTER(FileStats)]),
+        "vc_count_file_range": (C.c_int, [P, C.c_char_p, C.c_uint64, C.c_uint64, C.c_int, C.c_int,
+                                          C.POINTER(FileStats), C.POINTER(RangeInfo)]),
+        "vc_scan_file_range": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint64,
+                                         C.c_uint64, C.POINTER(FileStats), C.POINTER(RangeInfo), P, C.c_size_t,
+                                         P, C.c_size_t]),
+        "vc_ingest_profile": (C.c_uint64, [P]),
         "vc_scan_file": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(FileStats), P, C.c_size_t,
                                    P, C.c_size_t]),
         "vc_scan_file_parallel": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_uint64,
@@ -362,6 +380,18 @@ class KmerMap:
         _ck(rc, "vc_count_file(%s)" % fn)
         return st
 
+    def count_file_range(self, fn: str, begin: int, end: int, block_size: int = 10_000_000,
+                         n_thread: int = 4):
+        """One rank's byte range [begin, end) of a file (vc_count_file_range):
+        (FileStats, RangeInfo); FileNotFoundError if it cannot be opened."""
+        st, ri = FileStats(), RangeInfo()
+        rc = lib().vc_count_file_range(self._h, fn.encode(), begin, min(end, NO_OFFSET), block_size, n_thread,
+                                       C.byref(st), C.byref(ri))
+        if rc == VC_EIO:
+            raise FileNotFoundError(fn)
+        _ck(rc, "vc_count_file_range(%s)" % fn)
+        return st, ri
+
     def finish(self):
         """(counts uint32[2n], kmers_extracted) after all queued work."""
         counts = np.zeros(2 * self.n_patterns + 2, dtype=np.uint32)
@@ -512,6 +542,48 @@ def scan_file_parallel(fn: str, k: int, block_size: int = 10_000_000, threads: i
         raise FileNotFoundError(fn)
     _ck(rc, "vc_scan_file_parallel")
     return st, reads
+
+
+def scan_file_range(fn: str, k: int, begin: int, end: int, block_size: int = 10_000_000, threads: int = 4,
+                    piece_bytes: int = 8 << 20, with_reads: bool = False):
+    """Host-only: vc_count_file_range's reader over [begin, end) without a
+    device: (FileStats, RangeInfo, reads or None)."""
+    st, ri = FileStats(), RangeInfo()
+    end = min(end, NO_OFFSET)
+    if not with_reads:
+        rc = lib().vc_scan_file_range(fn.encode(), k, block_size, threads, piece_bytes, begin, end, C.byref(st),
+                                      C.byref(ri), None, 0, None, 0)
+        reads = None
+    else:
+        size = _text_size(fn) + 16
+        seq = np.zeros(max(size, 64), np.uint8)
+        lens = np.zeros(max(size, 16), np.uint32)
+        rc = lib().vc_scan_file_range(fn.encode(), k, block_size, threads, piece_bytes, begin, end, C.byref(st),
+                                      C.byref(ri), _ptr(seq), seq.size, _ptr(lens), lens.size)
+        reads = []
+        pos = 0
+        for i in range(int(st.seqs)):
+            n = int(lens[i])
+            reads.append(seq[pos:pos + n].tobytes())
+            pos += n
+    if rc == VC_EIO:
+        raise FileNotFoundError(fn)
+    _ck(rc, "vc_scan_file_range")
+    return st, ri, reads
+
+
+INGEST_PROFILE_KEYS = ("reader_s", "main_wait_s", "submit_s", "reparse_s", "parse_thread_s", "slot_wait_thread_s",
+                       "acquire_thread_s")
+
+
+def ingest_profile() -> dict:
+    """vc_ingest_profile: where this thread's last pass through the parallel
+    reader spent its time (seconds; *_thread_s summed over the workers)."""
+    out = np.zeros(7, np.float64)
+    n = lib().vc_ingest_profile(_ptr(out))
+    d = {k: round(float(v), 4) for k, v in zip(INGEST_PROFILE_KEYS, out)}
+    d["pieces"] = int(n)
+    return d
 
 
 def scan_records(fn: str, cap: int = 1 << 20) -> np.ndarray:

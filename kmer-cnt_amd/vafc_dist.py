@@ -1,7 +1,7 @@
 """One process per GPU: the drop-in vaf-counter as a torchrun job.
 
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
-        kmer-cnt_amd/vafc_dist.py [-v] -k 21 -p patterns.txt -o sample.vaf R1.fq.gz R2.fq.gz ...
+        kmer-cnt_amd/vafc_dist.py [-v] -k 21 -p patterns.txt -o sample.vaf R1.fq R2.fq.gz ...
 
 Same flags, messages, exit codes and .vaf as the reference's main
 (vaf-counter.c:584-735) and the drop-in CLI.  Reads are independent units, so
@@ -10,12 +10,19 @@ the path shards with no data-path collective:
 * every rank loads the patterns and builds its own replica of the static
   key table on its GPU (load_patterns / create_combined_kmer_map,
   vaf-counter.c:149-252);
-* input files are dealt round robin to the ranks (file i to rank i mod N) and
-  counted whole with vc_count_file.  A file is the unit because the
-  reference's block loop -- -b blocks in file order, a file ending at its
-  third empty block (vaf-counter.c:486-517, kthread.c:97-128) -- is a property
-  of one file's record sequence; splitting a file across processes would need
-  that state passed between them;
+* a plain FASTA/FASTQ file is split into N byte ranges, one per rank
+  (vc_count_file_range): rank r counts the records whose header lies in its
+  range, found from the record shape at the range's start as the parallel
+  reader's pieces are.  The reference reads the file in one kseq stream under
+  its block loop (vaf-counter.c:486-517, 550-582), so a split is exact only if
+  every range began at the record where the previous one ended and no range
+  met a truncated record (a -2 ends a block, and the file's end -- the third
+  empty block -- depends on the blocks before it).  The ranks exchange their
+  (first, next, errs) with one all-gather per file; if the chain does not
+  hold, every rank restores its counts from before the file and rank 0
+  counts the file whole, which is exactly vc_count_file;
+* gzip files (one deflate stream: no random access) are dealt whole, file
+  i to rank i mod N;
 * the per-rank uint32 count vectors and the tallies (valid k-mers, bases,
   sequences) are summed with ONE all-reduce each -- RCCL over xGMI with the
   "nccl" backend, gloo on CPU -- and rank 0 writes the .vaf and the -v report.
@@ -25,12 +32,15 @@ the path shards with no data-path collective:
   (vaf-counter.c:101-102,473-477), wrap-around included.
 
 The counting timer is the reference's (first file open to counts final),
-taken as the maximum over ranks after a barrier.  In-process multi-GPU (one
-process, several devices, one RCCL reduce inside vc_finish) is the drop-in
-CLI's VAFC_DEVICES (vc_create_multi); this module is the
-torchrun form of the same reduction, which is also what bench.py runs at
-N > 1.  The per-rank counter is pluggable (RankCounter): HipRankCounter is
-the product; the CPU tests run the same driver with the oracle.
+taken as the maximum over ranks after a barrier.  A rank whose counter fails
+(HIP error, out of memory) tells the others through the per-file all-gather
+or the agreement before the all-reduce, and every rank exits 1 -- no rank is
+left waiting in a collective.  In-process multi-GPU (one process, several
+devices, one RCCL reduce inside vc_finish) is the drop-in CLI's VAFC_DEVICES
+(vc_create_multi); this module is the torchrun form, which is
+also what bench.py runs at N > 1.  The per-rank counter is pluggable
+(RankCounter): HipRankCounter is the product; the CPU tests run the same
+driver with the oracle.
 """
 from __future__ import annotations
 
@@ -39,6 +49,9 @@ import sys
 import time
 
 import numpy as np
+
+NO_OFFSET = (1 << 64) - 1     # vc_range_info's UINT64_MAX ("none" / "the file ended")
+EMPTY_RANGE = NO_OFFSET - 1   # a rank whose nominal byte range is empty (more ranks than bytes)
 
 # --------------------------------------------------------------------------
 # sharding and the count reduction
@@ -55,6 +68,45 @@ def shard(n_items: int, rank: int, world: int):
 def deal(items, rank: int, world: int):
     """Round-robin share of a list (item i to rank i mod world), in order."""
     return [x for i, x in enumerate(items) if i % world == rank]
+
+
+def byte_range(size: int, rank: int, world: int):
+    """Rank's nominal byte range [begin, end) of a size-byte file; the last
+    range is open-ended (end = NO_OFFSET), so a file that grows is still read
+    to its end, as the reference would."""
+    begin = size * rank // world
+    end = NO_OFFSET if rank == world - 1 else size * (rank + 1) // world
+    return begin, end
+
+
+def splittable(fn: str) -> bool:
+    """A regular file that is not gzip (vc_count_file_range splits those only)."""
+    try:
+        if not os.path.isfile(fn):
+            return False
+        with open(fn, "rb") as f:
+            return f.read(2) != b"\x1f\x8b"
+    except OSError:
+        return False
+
+
+def chain_holds(infos) -> bool:
+    """infos[r] = (first, next, errs, stopped) of rank r's range, in rank order:
+    the ranges counted exactly the file's reads iff no range met a truncated
+    record and each range began where the previous one ended (vafc.h,
+    vc_count_file_range).  Empty ranges (EMPTY_RANGE) count nothing and are
+    passed over."""
+    infos = [i for i in infos if int(i[0]) != EMPTY_RANGE]
+    if not infos:
+        return True
+    if any(int(i[2]) != 0 for i in infos):
+        return False
+    if int(infos[0][0]) != 0 and int(infos[0][0]) != NO_OFFSET:
+        return False
+    for prev, cur in zip(infos, infos[1:]):
+        if int(cur[0]) != int(prev[1]):
+            return False
+    return True
 
 
 def counts_to_tensor(counts: np.ndarray, device="cpu"):
@@ -90,26 +142,53 @@ def allreduce_max(value: float, device="cpu", group=None) -> float:
     return float(t.item())
 
 
+def allgather_ints(values, world: int, device="cpu"):
+    """[values of rank 0, values of rank 1, ...]: one all-gather of a few
+    integers per rank (uint64 offsets travel as their int64 bit pattern)."""
+    import torch
+    import torch.distributed as dist
+    v = np.asarray(values, dtype=np.uint64).view(np.int64)
+    t = torch.from_numpy(v.copy()).to(device)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.cpu().numpy().view(np.uint64).tolist() for o in out]
+
+
 # --------------------------------------------------------------------------
 # per-rank counters
 # --------------------------------------------------------------------------
 
 
 class RankCounter:
-    """What a rank counts with: count_file for each of its files, then
+    """What a rank counts with: count_range for its share of each file, then
     local_counts gives its count vector (a tensor on `device`, where the
-    collective runs: the GPU with RCCL, "cpu" with gloo) and its k-mer tally."""
+    collective runs: the GPU with RCCL, "cpu" with gloo) and its k-mer tally.
+    save / restore bracket a split file whose ranges turn out not to chain."""
 
     device = "cpu"
 
-    def count_file(self, fn: str, block: int, threads: int):
-        """(ok, bases, seqs); ok False if the file cannot be opened (skipped
-        silently, as the reference does, vaf-counter.c:557)."""
+    def count_range(self, fn: str, begin: int, end: int, block: int, threads: int):
+        """(ok, bases, seqs, (first, next, errs, stopped)) of the records of fn
+        whose header lies in [first, end) (vafc.h vc_count_file_range); ok
+        False if the file cannot be opened (skipped silently, as the reference
+        does, vaf-counter.c:557).  begin = 0, end = NO_OFFSET: the whole file."""
+        raise NotImplementedError
+
+    def save(self):
+        """Remember the counts and the k-mer tally (before a split file)."""
+        raise NotImplementedError
+
+    def restore(self):
+        """Return to the counts and tally of the last save()."""
         raise NotImplementedError
 
     def local_counts(self):
         """This rank's (counts tensor on self.device, kmers)."""
         raise NotImplementedError
+
+    def table_info(self):
+        """The key table's geometry for the -v report (vc_table_info)."""
+        return {"n_keys": 0, "slots": 0, "filter_bytes": 0}
 
     def close(self):
         pass
@@ -126,23 +205,44 @@ class HipRankCounter(RankCounter):
         import vafc
         self.torch = torch
         self.dev = torch.device("cuda", local_rank)
-        self.map = vafc.create_combined_kmer_map(db, k, device=local_rank)
+        keys, vals, _ = db.keys(k)
+        # the map without create_combined_kmer_map's warning: run() prints it once, on rank 0
+        self.map = vafc.KmerMap(k, keys, vals, db.n, local_rank)
         self.counts = torch.zeros(2 * db.n, dtype=torch.int32, device=self.dev)
         self.tally = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        # the zero fills run on torch's stream, the counting kernels on the
+        # map's own stream: finish the fills before the first count
+        torch.cuda.current_stream(self.dev).synchronize()
         self.map.bind_outputs(self.counts.data_ptr(), self.tally.data_ptr())
         self.device = self.dev if backend == "nccl" else "cpu"
+        self._saved = None
 
-    def count_file(self, fn, block, threads):
+    def count_range(self, fn, begin, end, block, threads):
         try:
-            st = self.map.count_file(fn, block, threads)
+            st, ri = self.map.count_file_range(fn, begin, end, block, threads)
         except FileNotFoundError:
-            return False, 0, 0
-        return True, st.bases, st.seqs
+            return False, 0, 0, (NO_OFFSET, NO_OFFSET, 0, 0)
+        return True, st.bases, st.seqs, (ri.first, ri.next, ri.errs, ri.stopped)
+
+    def save(self):
+        # count_file_range returns after the map's stream is synchronised, so
+        # the counts are final; the copies run on torch's stream and are
+        # finished before the next count
+        self._saved = (self.counts.clone(), self.tally.clone())
+        self.torch.cuda.current_stream(self.dev).synchronize()
+
+    def restore(self):
+        self.counts.copy_(self._saved[0])
+        self.tally.copy_(self._saved[1])
+        self.torch.cuda.current_stream(self.dev).synchronize()
 
     def local_counts(self):
         self.map.finish()                     # the rank's batches are all counted (syncs its stream)
         t = self.counts if self.device != "cpu" else self.counts.cpu()
         return t, int(self.tally.item())
+
+    def table_info(self):
+        return self.map.table_info()
 
     def close(self):
         self.map.bind_outputs(0, 0)
@@ -163,6 +263,74 @@ def _agree(ok: bool, world: int, device) -> bool:
     t = torch.tensor([0 if ok else 1], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return int(t.item()) == 0
+
+
+def _khashl_capacity(n: int) -> int:
+    """The reference's hash table capacity for n patterns (3n rounded up to a
+    power of two, at least 4), as the drop-in CLI reports it."""
+    want = 3 * n
+    bits = max(want.bit_length() - 1 + (1 if want & (want - 1) else 0), 2)
+    return 1 << bits
+
+
+def count_files(files, counter, o, rank, world, err, coll_device):
+    """The reference's per-file loop (vaf-counter.c:644-650) over the ranks:
+    (ok, bases, seqs, fallbacks).  ok is False on every rank as soon as any
+    rank's counter failed."""
+    bases = seqs = fallbacks = 0
+    ok = True
+    for i, fn in enumerate(files):
+        if rank == 0:
+            err("[M::main] Processing %s...\n" % fn)
+        if world > 1 and splittable(fn):
+            size = os.path.getsize(fn)
+            begin, end = byte_range(size, rank, world)
+            counter.save()
+            failed = False
+            try:
+                if end <= begin:     # an empty share: nothing to count (chain_holds passes over it)
+                    good, b, s, info = True, 0, 0, (EMPTY_RANGE, EMPTY_RANGE, 0, 0)
+                else:
+                    good, b, s, info = counter.count_range(fn, begin, end, o["b"], o["t"])
+            except Exception as e:   # VafcError (HIP, memory): tell the other ranks first
+                err("Error: counting failed on %s (%s)\n" % (fn, e))
+                failed, good, b, s, info = True, False, 0, 0, (NO_OFFSET, NO_OFFSET, 0, 0)
+            rows = allgather_ints(list(info) + [1 if good else 0, 1 if failed else 0], world, coll_device)
+            if any(r[5] for r in rows):
+                ok = False
+                break
+            if not any(r[4] for r in rows):   # the file vanished: skipped, as the reference does
+                continue
+            if chain_holds([r[:4] for r in rows]):
+                bases += b
+                seqs += s
+                continue
+            # not an exact split (a truncated record, a mis-guessed boundary):
+            # rank 0 counts the file whole, the others forget their share
+            fallbacks += 1
+            counter.restore()
+            if rank == 0:
+                try:
+                    good, b, s, _ = counter.count_range(fn, 0, NO_OFFSET, o["b"], o["t"])
+                    if good:
+                        bases += b
+                        seqs += s
+                except Exception as e:
+                    err("Error: counting failed on %s (%s)\n" % (fn, e))
+                    ok = False
+            continue
+        if i % world != rank:        # whole files (gzip, or one rank) dealt round robin
+            continue
+        try:
+            good, b, s, _ = counter.count_range(fn, 0, NO_OFFSET, o["b"], o["t"])
+        except Exception as e:
+            err("Error: counting failed on %s (%s)\n" % (fn, e))
+            ok = False
+            continue
+        if good:
+            bases += b
+            seqs += s
+    return ok, bases, seqs, fallbacks
 
 
 def run(argv, make_counter, rank: int = 0, world: int = 1, err=None, coll_device="cpu") -> int:
@@ -213,24 +381,31 @@ def run(argv, make_counter, rank: int = 0, world: int = 1, err=None, coll_device
         db.close()
         return 1
     t_map = time.time() - t
+    tinfo = counter.table_info()
+    n_entries = int(tinfo.get("n_keys") or keys.size)
     if o["v"] and rank == 0:
-        err("[V::main] Created k-mer map with %d entries in %.3f sec\n" % (keys.size, t_map))
+        err("[V::main] Created k-mer map with %d entries in %.3f sec\n" % (n_entries, t_map))
     if rank == 0:
         err("[M::main] Counting k-mers in FASTQ files with %d threads...\n" % o["t"])
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
     t = time.time()
-    bases = seqs = 0
-    mine = deal(list(range(len(files))), rank, world)
-    for i in mine:
-        fn = files[i]
-        err("[M::main] Processing %s...\n" % fn)
-        ok, b, s = counter.count_file(fn, o["b"], o["t"])
-        if ok:
-            bases += b
-            seqs += s
-    counts_t, km = counter.local_counts()
+    ok, bases, seqs, _ = count_files(files, counter, o, rank, world, err, coll_device)
+    counts_t = None
+    km = 0
+    if ok:
+        try:
+            counts_t, km = counter.local_counts()
+        except Exception as e:
+            err("Error: counting failed (%s)\n" % e)
+            ok = False
+    if not _agree(ok, world, coll_device):
+        if rank == 0:
+            err("Error: counting failed\n")
+        counter.close()
+        db.close()
+        return 1
     if world > 1:
         allreduce_counts(counts_t)
         km = allreduce_u64(km, counter.device)
@@ -255,10 +430,13 @@ def run(argv, make_counter, rank: int = 0, world: int = 1, err=None, coll_device
         t_write = time.time() - t
         if rc == 0:
             err("[M::main] Done. Average depth: %.2f\n" % avg)
-        if rc == 0 and o["v"]:
+        if rc == 0 and o["v"]:   # the reference's report, vaf-counter.c:686-729
             total = time.time() - t_start
+            cap = _khashl_capacity(db.n)
             err("\n=== Performance Statistics ===\n")
             err("Total runtime:           %.3f sec\n" % total)
+            err("  Pattern loading:       %.3f sec (%.1f%%)\n" % (t_load, 100.0 * t_load / total))
+            err("  K-mer map creation:    %.3f sec (%.1f%%)\n" % (t_map, 100.0 * t_map / total))
             err("  K-mer counting:        %.3f sec (%.1f%%)\n" % (t_count, 100.0 * t_count / total))
             err("  Output writing:        %.3f sec (%.1f%%)\n" % (t_write, 100.0 * t_write / total))
             err("\nThroughput:\n")
@@ -268,7 +446,15 @@ def run(argv, make_counter, rank: int = 0, world: int = 1, err=None, coll_device
             if t_count > 0:
                 err("  Speed:                 %.2f Mbases/sec\n" % (bases / t_count / 1e6))
                 err("  K-mer throughput:      %.2f million k-mers/sec\n" % (km / t_count / 1e6))
-            err("  Ranks:                 %d (files dealt round robin, one all-reduce of the counts)\n" % world)
+            err("\nMemory:\n")
+            err("  Patterns:              %d\n" % db.n)
+            err("  Hash table entries:    %d\n" % n_entries)
+            err("  Hash table capacity:   %d\n" % cap)
+            err("  Hash table load:       %.1f%%\n" % (100.0 * n_entries / cap))
+            err("\nOptimizations:\n")
+            err("  SIMD:                  MI355X HIP (gfx950), LDS prefilter %d KiB, device table %d slots\n"
+                % (int(tinfo.get("filter_bytes", 0)) >> 10, int(tinfo.get("slots", 0))))
+            err("  Threads:               %d workers\n" % o["t"])
             err("==============================\n")
     db.close()
     if world > 1:

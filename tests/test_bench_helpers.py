@@ -77,3 +77,44 @@ def test_vaf_counts_reads_the_writer_output(tmp_path):
     counts = np.random.default_rng(1).integers(0, 2 ** 32, 2 * db.n, dtype=np.uint64).astype(np.uint32)
     db.write_vaf(counts, str(tmp_path / "o.vaf"))
     assert np.array_equal(bench.vaf_counts(str(tmp_path / "o.vaf")), counts)
+
+
+def test_bench_spawns_one_rank_per_gpu(tmp_path):
+    """`bench.py --gpus N` outside torchrun starts N rank processes with the
+    torchrun environment (rank 0's stdout is the bench's), and returns the
+    first failing rank's status after stopping the others."""
+    import subprocess
+    import sys
+    import bench
+    child = tmp_path / "child.py"
+    child.write_text("import os, sys, time\n"
+                     "r = int(os.environ['RANK'])\n"
+                     "print('rank', r, os.environ['LOCAL_RANK'], os.environ['WORLD_SIZE'], os.environ['MASTER_ADDR'],"
+                     " flush=True)\n"
+                     "if 'fail' in sys.argv and r == 1: sys.exit(3)\n"
+                     "if 'fail' in sys.argv: time.sleep(30)\n")
+    out = subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, %r); import bench; "
+                          "sys.exit(bench.spawn_ranks(['x'], 3, %r))" % (os.path.dirname(bench.__file__), str(child))],
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0
+    assert out.stdout.split() == ["rank", "0", "0", "3", "127.0.0.1"]          # only rank 0 prints
+    import time
+    t0 = time.time()
+    assert bench.spawn_ranks(["fail"], 2, str(child)) == 3
+    assert time.time() - t0 < 20                                                # rank 0 was stopped
+
+
+def test_bench_refuses_world_size_other_than_gpus():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode == 2 and "WORLD_SIZE" in p.stderr and p.stdout == ""
+
+
+def test_rank_threads_split_the_share():
+    import bench
+    assert 1 <= bench.rank_threads(1) <= 16
+    assert bench.rank_threads(8) <= max(1, bench.rank_threads(1))

@@ -432,6 +432,28 @@ def test_large_panel_c5_shape():
     assert int(got.sum()) > 20_000
 
 
+def _oracle_windows(m, orc, d_seq, d_offs, d_lens, R, L, n=1_000_000):
+    """Full-size parity past the prefix (the per-read loop being replaced is
+    vaf-counter.c:349-427): windows of n reads counted in place -- the whole
+    HBM buffer as the read bytes, the offsets and lengths from read j on, so
+    the kernel addresses the reads by their absolute byte offsets -- against
+    the oracle on the same reads copied out.  The windows: the one straddling
+    byte offset 2^32, one in the middle (not aligned to anything), the last n
+    reads (offsets near the end, above 4 GiB for every full-size config).
+    Returns the windows checked."""
+    js = sorted({max(0, min(R - n, (1 << 32) // L - n // 2)), max(0, min(R - n, R // 2 + 12_345)), R - n})
+    for j in js:
+        m.reset()
+        m.count_device(d_seq.data_ptr(), R * L, d_offs.data_ptr() + 8 * j, d_lens.data_ptr() + 4 * j, n)
+        c, km = m.finish()
+        seq = d_seq[j * L:(j + n) * L].cpu().numpy()
+        want, km_want = orc.count_reads(seq, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint32))
+        assert km == km_want, (j, km, km_want)
+        assert np.array_equal(c, want), (j, int((c != want).sum()))
+    assert (R - n) * L > (1 << 32) or R * L <= (1 << 32)
+    return js
+
+
 FULL_SIZE = {   # BASELINE.json configs at their full size on one GPU
     "c2": (21, "grch38", 100_000_000),    # 100M reads, ~20k SNPs
     "c3": (31, "grch38", 200_000_000),    # 100M pairs = 200M reads, k = 31
@@ -442,8 +464,9 @@ FULL_SIZE = {   # BASELINE.json configs at their full size on one GPU
 @pytest.mark.parametrize("config", sorted(FULL_SIZE))
 def test_full_size_linearity_and_prefix_parity(torch_dev, config):
     """At BASELINE size (HBM-resident): count(all) == count(first half) +
-    count(second half) (mod 2^32), k-mer tallies add up, and an exact 1M-read prefix
-    matches the oracle."""
+    count(second half) (mod 2^32), k-mer tallies add up, and exact 1M-read
+    windows -- the prefix, across byte offset 2^32, the middle, the last reads --
+    match the oracle."""
     import torch
     import vafc
     import vafc_synth as S
@@ -490,6 +513,7 @@ def test_full_size_linearity_and_prefix_parity(torch_dev, config):
     seq = d_seq[: n * L].cpu().numpy()
     want, km_want = orc.count_reads(seq, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint32))
     assert p_k == km_want and np.array_equal(p_c, want)
+    _oracle_windows(m, orc, d_seq, d_offs, d_lens, R, L)
     m.close()
 
 
@@ -547,7 +571,8 @@ def test_c4_full_size_sharded(torch_dev):
     vc_create_multi(devices=[0, 0]) -- the two halves dealt to the two shards by
     vc_count_device, summed on the device by vc_finish -- the totals are equal
     (linearity: all = first half + second half, mod 2^32), the k-mer tallies add
-    up, and an exact 1M-read prefix matches the oracle.  The reference counts
+    up, and exact 1M-read windows (the prefix, across 2^32, the middle, the
+    last reads at 148 GB) match the oracle.  The reference counts
     every block of every file into one set of u32 counters
     (vaf-counter.c:473-477,647-650); sharding must not change them."""
     import torch
@@ -601,6 +626,7 @@ def test_c4_full_size_sharded(torch_dev):
     seq = d_seq[: n * L].cpu().numpy()
     want, km_want = orc.count_reads(seq, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint32))
     assert p_k == km_want and np.array_equal(p_c, want)
+    _oracle_windows(one, orc, d_seq, d_offs, d_lens, R, L)
     one.close()
     two.close()
     del d_seq, d_offs, d_lens

@@ -126,3 +126,105 @@ def test_gzip_goes_to_the_inflater(tmp_path):
         f.write(b"@a\nACGT\n+\nIIII\n")
     st, reads = vafc.scan_file_parallel(p, 3, with_reads=True)
     assert reads == [b"ACGT"] and st.bases == 4
+
+
+# --------------------------------------------------------------------------
+# byte ranges (vc_scan_file_range, the reader of vc_count_file_range): one
+# rank's share of a file in the torchrun driver (kmer-cnt_amd/vafc_dist.py)
+# --------------------------------------------------------------------------
+
+def _ranges(path, k, b, cuts, threads=2, piece=4096):
+    """Scan [0, c1), [c1, c2), ..., [cn, end) and apply vafc_dist's chain rule."""
+    import vafc
+    import vafc_dist as D
+    bounds = [0] + sorted(cuts) + [D.NO_OFFSET]
+    infos, reads, bases, seqs = [], [], 0, 0
+    for a, e in zip(bounds, bounds[1:]):
+        if e <= a:
+            infos.append((D.EMPTY_RANGE, D.EMPTY_RANGE, 0, 0))
+            continue
+        st, ri, r = vafc.scan_file_range(path, k, a, e, b, threads, piece, with_reads=True)
+        assert ri.whole == 0
+        infos.append((ri.first, ri.next, ri.errs, ri.stopped))
+        reads += r
+        bases += st.bases
+        seqs += st.seqs
+    return D.chain_holds(infos), infos, reads, bases, seqs
+
+
+@pytest.mark.parametrize("crlf", [False, True])
+@pytest.mark.parametrize("n_cuts", [1, 2, 7])
+def test_ranges_of_clean_fastq_chain_and_equal_the_whole_file(tmp_path, crlf, n_cuts):
+    """Well-formed FASTQ cut at arbitrary bytes (inside headers, sequences,
+    '+' lines and qualities): every range finds the record where the previous
+    one stopped, and the ranges' reads are the whole file's, in order."""
+    import vafc
+    rng = np.random.default_rng(11 + n_cuts)
+    p = str(tmp_path / "clean.fq")
+    _fastq(p, rng, 3000, crlf=crlf)
+    st0, r0 = vafc.scan_file(p, 21, 10_000, with_reads=True)
+    size = os.path.getsize(p)
+    for trial in range(6):
+        cuts = rng.integers(1, size, n_cuts).tolist()
+        ok, infos, reads, bases, seqs = _ranges(p, 21, 10_000, cuts, piece=int(rng.integers(50, 5000)))
+        assert ok, infos
+        assert reads == r0 and (bases, seqs) == (st0.bases, st0.seqs)
+
+
+def test_range_edges(tmp_path):
+    """A range that starts past the end or inside the last record counts
+    nothing (first = next = the end); an empty file; a range at offset 0 is
+    the whole-file reader's prefix."""
+    import vafc
+    import vafc_dist as D
+    rng = np.random.default_rng(5)
+    p = str(tmp_path / "c.fq")
+    _fastq(p, rng, 50)
+    size = os.path.getsize(p)
+    st, ri, reads = vafc.scan_file_range(p, 21, size + 10, D.NO_OFFSET, with_reads=True)
+    assert (ri.first, ri.next, st.seqs) == (D.NO_OFFSET, D.NO_OFFSET, 0)
+    st, ri, reads = vafc.scan_file_range(p, 21, size - 20, D.NO_OFFSET, with_reads=True)
+    assert ri.first == D.NO_OFFSET and st.seqs == 0
+    st, ri, reads = vafc.scan_file_range(p, 21, 0, 1, with_reads=True)
+    assert ri.first == 0 and st.seqs == 1 and ri.next > 0 and ri.next < size
+    st2, ri2, _ = vafc.scan_file_range(p, 21, 1, D.NO_OFFSET, with_reads=True)
+    assert ri2.first == ri.next and st.seqs + st2.seqs == 50 and ri2.next == D.NO_OFFSET and ri2.stopped
+    e = str(tmp_path / "empty.fq")
+    open(e, "wb").close()
+    st, ri, _ = vafc.scan_file_range(e, 21, 0, D.NO_OFFSET, with_reads=True)
+    assert st.seqs == 0 and ri.first == D.NO_OFFSET
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_ranges_of_fuzzed_inputs_are_exact_or_refused(seed, tmp_path):
+    """Malformed and odd inputs: whenever vafc_dist's chain rule accepts a
+    split, its reads and tallies equal the whole file's; a split it refuses
+    falls back to one whole-file range (which is vc_count_file)."""
+    import vafc
+    rng = np.random.default_rng(1300 + seed)
+    p = str(tmp_path / "fuzz.fq")
+    _fuzz_file(p, rng, 300)
+    size = os.path.getsize(p)
+    for k, b in ((5, 10_000_000), (5, 1), (12, 50)):
+        st0, r0 = vafc.scan_file(p, k, b, with_reads=True)
+        for trial in range(4):
+            cuts = rng.integers(1, size, 1 + trial).tolist()
+            ok, infos, reads, bases, seqs = _ranges(p, k, b, cuts, threads=1 + seed % 3,
+                                                    piece=int(rng.integers(7, 700)))
+            if ok:
+                assert reads == r0 and (bases, seqs) == (st0.bases, st0.seqs), (k, b, cuts, infos)
+
+
+def test_ranges_of_gzip_are_whole(tmp_path):
+    """gzip is not split: begin 0 reads the whole file, later ranges nothing."""
+    import gzip
+    import vafc
+    import vafc_dist as D
+    p = str(tmp_path / "x.fq.gz")
+    with gzip.open(p, "wb") as f:
+        f.write(b"@a\nACGTACGT\n+\nIIIIIIII\n" * 10)
+    st, ri, reads = vafc.scan_file_range(p, 3, 0, 5, with_reads=True)
+    assert ri.whole == 1 and st.seqs == 10 and ri.next == D.NO_OFFSET
+    st, ri, reads = vafc.scan_file_range(p, 3, 5, D.NO_OFFSET, with_reads=True)
+    assert ri.whole == 1 and st.seqs == 0 and ri.first == D.NO_OFFSET
+    assert not D.splittable(p)

@@ -135,7 +135,11 @@ def test_cli_option_parsing_mirror():
 # one all-reduce, rank 0 writes the .vaf -- against the reference's goldens
 # --------------------------------------------------------------------------
 
-DIST_CASES = ["pe_k31", "c1_plumbing_k21", "missing_file", "mal_gbbbgbbbg_b1", "pal_k16"]
+DIST_CASES = ["pe_k31", "c1_plumbing_k21", "c1_plumbing_k21_gz", "c1_k21_b1", "missing_file", "multiline_k21",
+              "edge_crlf_k21", "pat_edge_k31", "truncated", "empty_reads", "mal_gbbbgbbbg_b1", "mal_bg", "pal_k16"]
+# cases whose every file is well formed and plain: the byte ranges must chain
+# (no fallback to a whole-file recount)
+DIST_CLEAN = {"pe_k31", "c1_plumbing_k21", "c1_k21_b1", "pal_k16"}
 
 
 def _driver_rank(rank, world, port, argv, cwd, out_json, counter):
@@ -149,21 +153,50 @@ def _driver_rank(rank, world, port, argv, cwd, out_json, counter):
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     os.chdir(cwd)
     lines = []
+    calls = {"ranges": 0, "whole": 0, "restores": 0}
 
     class OracleRankCounter(D.RankCounter):     # CPU stand-in for the per-GPU counter (test infrastructure)
+        """The oracle counts what the product's host-only range reader
+        (vc_scan_file_range) hands it; whole files through the oracle's own
+        reader and block loop."""
+
         def __init__(self, db, k):
             import oracle as O
+            self.k = k
             self.n = db.n
             self.orc = O.Oracle(k, pattern_fn=argv[argv.index("-p") + 1])
             self.counts = np.zeros(2 * db.n + 2, np.uint32)
             self.km = 0
 
-        def count_file(self, fn, block, threads):
-            rc, b, s, km = self.orc.count_file(fn, block, self.counts)
-            if rc != 0:
-                return False, 0, 0
-            self.km += km
-            return True, b, s
+        def count_range(self, fn, begin, end, block, threads):
+            import vafc
+            if begin == 0 and end == D.NO_OFFSET:
+                calls["whole"] += 1
+                rc, b, s, km = self.orc.count_file(fn, block, self.counts)
+                if rc != 0:
+                    return False, 0, 0, (D.NO_OFFSET, D.NO_OFFSET, 0, 0)
+                self.km += km
+                return True, b, s, (0, D.NO_OFFSET, 0, 1)
+            calls["ranges"] += 1
+            try:
+                st, ri, reads = vafc.scan_file_range(fn, self.k, begin, end, block, threads, 64, with_reads=True)
+            except FileNotFoundError:
+                return False, 0, 0, (D.NO_OFFSET, D.NO_OFFSET, 0, 0)
+            if reads:
+                lens = np.array([len(r) for r in reads], np.uint32)
+                offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+                seq = np.frombuffer(b"".join(reads), np.uint8)
+                c, km = self.orc.count_reads(seq, offs, lens, self.n)
+                self.counts[:2 * self.n] += c
+                self.km += km
+            return True, st.bases, st.seqs, (ri.first, ri.next, ri.errs, ri.stopped)
+
+        def save(self):
+            self._saved = (self.counts.copy(), self.km)
+
+        def restore(self):
+            calls["restores"] += 1
+            self.counts, self.km = self._saved[0].copy(), self._saved[1]
 
         def local_counts(self):
             return D.counts_to_tensor(self.counts[:2 * self.n]), self.km
@@ -175,7 +208,7 @@ def _driver_rank(rank, world, port, argv, cwd, out_json, counter):
 
     rc = D.run(argv, make, rank, world, err=lines.append)
     with open(out_json + ".%d" % rank, "w") as f:
-        json.dump({"rc": rc, "stderr": "".join(lines)}, f)
+        json.dump({"rc": rc, "stderr": "".join(lines), "calls": calls}, f)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -200,24 +233,36 @@ def _run_driver(entry, synth_dir, tmp_path, counter, world=2):
             if pat in line:
                 stats[key] = int(line.split(":")[1].split()[0])
     data = open(out, "rb").read() if os.path.exists(out) else None
-    return [r["rc"] for r in ranks], stats, data, ranks[0]["stderr"]
+    return [r["rc"] for r in ranks], stats, data, ranks[0]["stderr"], [r.get("calls") for r in ranks]
 
 
 @pytest.mark.parametrize("counter", ["oracle", pytest.param("hip", marks=pytest.mark.gpu)])
-@pytest.mark.parametrize("name", DIST_CASES)
-def test_dist_driver_matches_reference(name, counter, manifest, synth_dir, tmp_path):
-    """vafc_dist.run over two gloo ranks (the oracle as the per-rank counter on
-    CPU; the HIP counter, both ranks on device 0, in the GPU suite): the files
-    are dealt over the ranks, the counts all-reduced, and rank 0's .vaf and -v
-    tallies equal the reference's."""
+@pytest.mark.parametrize("name,world", [(n, 2) for n in DIST_CASES] + [("c1_plumbing_k21", 3), ("pe_k31", 3),
+                                                                       ("mal_bg", 3)])
+def test_dist_driver_matches_reference(name, world, counter, manifest, synth_dir, tmp_path):
+    """vafc_dist.run over gloo ranks (the oracle as the per-rank counter on
+    CPU; the HIP counter, every rank on device 0, in the GPU suite): plain
+    files split into byte ranges over the ranks, gzip files dealt whole, the
+    counts all-reduced; rank 0's .vaf and -v tallies equal the reference's.
+    Well-formed plain files must split without a fallback; the malformed ones
+    must fall back to a whole-file recount on rank 0."""
     import hashlib
     entry = next(c for c in manifest["cases"] if c["name"] == name)
-    rcs, stats, data, err = _run_driver(entry, synth_dir, tmp_path, counter)
-    assert rcs == [entry["exit"]] * 2, err[-2000:]
+    rcs, stats, data, err, calls = _run_driver(entry, synth_dir, tmp_path, counter, world)
+    assert rcs == [entry["exit"]] * world, err[-2000:]
     assert hashlib.md5(data).hexdigest() == entry["vaf_md5"]
     for key in ("bases", "seqs", "kmers"):
         assert stats.get(key) == entry["stats"].get(key), key
-    assert ("collisions detected" in err) == entry["collision_warning"]
+    assert err.count("collisions detected") == (1 if entry["collision_warning"] else 0)
+    # the reference's message sequence on rank 0: one Processing line per input, in argv order
+    inputs = [a for a in entry["argv"] if a.endswith((".fq", ".gz", ".fa"))]
+    assert [ln.split("Processing ")[1][:-3] for ln in err.splitlines() if "Processing " in ln] == inputs
+    assert "Ranks:" not in err
+    if counter == "oracle":
+        if name in DIST_CLEAN:
+            assert all(c["restores"] == 0 and c["ranges"] >= 1 for c in calls), calls
+        if name.startswith("mal_") or name == "truncated":
+            assert all(c["restores"] >= 1 for c in calls), calls
 
 
 def test_dist_driver_usage_and_missing_patterns(tmp_path):

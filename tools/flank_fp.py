@@ -10,7 +10,7 @@ the four-test one of the kernels (distances VC_FLANK_DIST(k, 0..3)).  Each is
 queried with 4M uniform random k-mers and with the valid windows of 200k
 benchmark reads (C2's generator: 1 % of reads drawn over a SNP, so some
 passes are true hits; "true" = windows that are keys).
-    python tools/flank_fp.py [--extra]
+    python tools/flank_fp.py [--extra | --sampled]
 """
 import os
 import sys
@@ -114,8 +114,51 @@ def extra_tests():
         print("k=21 distances=%s density %.3f reads %.4f%%" % (ds, bm.mean(), 100 * ok.mean()))
 
 
+
+
+def sampled_tests():
+    """Round 5: a content-sampled flank filter.  Each
+    10-mer is 'sampled' iff a hash of it is 0 mod s (the same rule on the read
+    and on the key, so a key's sampled 10-mers are its window's); S holds the
+    sampled 10-mers of every key orientation; a window passes iff every
+    sampled 10-mer inside it is in S -- and a window with none inside must
+    pass (nothing to test).  Prints the pass rate on the benchmark reads and
+    the share of windows with no sampled 10-mer, per s."""
+    panel = S.make_panel(S.read_bed(S.default_bed_path()))
+    reads = S.gen_reads(panel, 200_000)
+    K = 21
+    d = tempfile.mkdtemp()
+    pat = os.path.join(d, "p.txt")
+    panel.write_patterns(pat, K)
+    keys, _, _ = vafc.load_patterns(pat).keys(K)
+    keys = np.unique(np.asarray(keys, dtype=np.uint64))
+    allk = np.concatenate([keys, revcomp(keys, K)])
+    win = read_windows(reads, K)
+
+    def h(v):
+        return ((v * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(40)) & np.uint64(0xFFFFFF)
+
+    for s in (2, 3, 4, 6):
+        bm = np.zeros(1 << 20, bool)
+        for dd in range(K - 9):
+            v = (allk >> np.uint64(2 * dd)) & M
+            sel = (h(v) % np.uint64(s)) == 0
+            bm[v[sel]] = True
+        ok = np.ones(win.size, bool)
+        nsamp = np.zeros(win.size, np.int64)
+        for dd in range(K - 9):
+            v = (win >> np.uint64(2 * dd)) & M
+            sel = (h(v) % np.uint64(s)) == 0
+            nsamp += sel
+            ok &= ~sel | bm[v]
+        print("k=21 sampled 1/%d: density %.3f, windows with no sampled 10-mer %.3f%%, pass %.4f%%" % (
+            s, bm.mean(), 100 * (nsamp == 0).mean(), 100 * ok.mean()))
+
+
 if __name__ == "__main__":
     if "--extra" in sys.argv:
         extra_tests()
+    elif "--sampled" in sys.argv:
+        sampled_tests()
     else:
         main()

@@ -7,7 +7,8 @@ uniform random 21-mers:
   canon   word / bits from vc_hash / vc_hash2 of the canonical k-mer (round 1:
           the drain reverse-complements every queued k-mer and hashes it)
   strands word / bits from a symmetric mix of the two strands' low 32 bits,
-          (flo, rlo), which the scan already has (vafc_common.h vc_l2f_*)
+          (flo, rlo), which the scan already has (round 2's form)
+  l2s     round 5's form of the same (vafc_common.h vc_l2s_hash*, -DVC_BIG_SYMQ)
     python tools/l2f_fp.py
 """
 import os
@@ -70,6 +71,20 @@ def strands_filter(keys, l2bits):
     return w >> np.uint32(32 - l2bits), mask3(b >> np.uint32(17))
 
 
+def l2s_filter(keys, l2bits):
+    """vafc_common.h vc_l2s_hash / vc_l2s_hash2 (round 5, -DVC_BIG_SYMQ): two
+    multiplies of the strands' low words, summed / XORed, then mixed."""
+    m = np.uint32(0x9E3779B1)
+    u, v = m32(keys) * m, m32(revcomp(keys)) * m
+    x = u + v
+    x ^= x >> np.uint32(15)
+    x = x * np.uint32(0x85EBCA77)
+    y = u ^ v
+    y ^= y >> np.uint32(13)
+    y = y * np.uint32(0xC2B2AE3D)
+    return x >> np.uint32(32 - l2bits), mask3(y)
+
+
 def fp(fn, keys, q, l2bits):
     words = np.zeros(1 << l2bits, np.uint32)
     w, m = fn(keys, l2bits)
@@ -93,7 +108,7 @@ def main():
     q = np.random.default_rng(1).integers(0, 1 << (2 * K), size=2_000_000, dtype=np.uint64)
     q = np.minimum(q, revcomp(q))
     print("%d keys, 2^%d words (%.1f bits per key)" % (keys.size, l2bits, 32 * (1 << l2bits) / keys.size))
-    for name, fn in (("canon", canon_filter), ("strands", strands_filter)):
+    for name, fn in (("canon", canon_filter), ("strands", strands_filter), ("l2s", l2s_filter)):
         print("%-8s FP %.4f %%" % (name, 100 * fp(fn, keys, q, l2bits)))
 
 
