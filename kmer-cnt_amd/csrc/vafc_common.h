@@ -126,10 +126,10 @@ VC_HD uint32_t vc_l2f_mask(uint32_t h2)
 }
 
 /* The same filter keyed by the two strands' low 32 bits instead of the
- * canonical k-mer (build option VC_BIG_SYMQ, large-panel kernels only): the
- * queue then holds (rlo << 32) | flo, which the drain tests with two
- * multiplies and no reverse complement; only survivors rebuild the canonical
- * k-mer (vc_canon_from_strands).  Symmetric in (flo, rlo), so it is a
+ * canonical k-mer (the large-panel kernels, VC_KV_BIG; -DVC_BIG_RAWQ restores
+ * the round-4 form for A/B): the queue holds (rlo << 32) | flo, which the drain
+ * tests with two multiplies and no reverse complement; only survivors rebuild
+ * the canonical k-mer (vc_canon_from_strands).  Symmetric in (flo, rlo), so it is a
  * function of the canonical k-mer.  Word from the top bits of one mix, bits
  * from a second one. */
 VC_HD uint32_t vc_l2s_hash(uint32_t flo, uint32_t rlo)

@@ -232,6 +232,7 @@ struct Slot {
 	uint32_t *d_lens = nullptr;
 	size_t cap_bytes = 0, cap_reads = 0;
 	hipEvent_t done = nullptr;
+	hipEvent_t copied = nullptr;  // parallel reader: the slot's H2D copies (copy stream) are done
 	bool pending = false;
 };
 
@@ -269,6 +270,8 @@ struct vc_ctx {
 	Slot slot[2];
 	int cur = 0;
 	std::vector<Slot> islot;               // parallel ingest (vc_count_file on plain files)
+	hipStream_t cst = nullptr;             // the parallel reader's H2D copies (created on first use)
+	bool ingest_warm = false;              // a parallel-reader pass has completed: its slots are pinned
 	bool timing = false, timed = false;
 	hipEvent_t t0 = nullptr, t1 = nullptr;
 	// vc_count_device on a stream other than st: st's work so far -> that
@@ -400,7 +403,7 @@ extern "C" int vc_create(vc_ctx **out, int k, const uint64_t *keys, const uint32
 			fw.swap(fbig);
 			c->big = 1;
 			c->qcap = VC_BIG_QCAP;
-#ifdef VC_BIG_SYMQ
+#ifndef VC_BIG_RAWQ
 			// the big kernels queue both strands' low words: key the second
 			// level by them (vc_l2s_*) instead of the canonical k-mer
 			std::fill(l2w.begin(), l2w.end(), 0u);
@@ -514,7 +517,9 @@ extern "C" void vc_destroy(vc_ctx *c)
 	for (auto &s : c->islot) {
 		free_slot(s);
 		if (s.done) (void)hipEventDestroy(s.done);
+		if (s.copied) (void)hipEventDestroy(s.copied);
 	}
+	if (c->cst) (void)hipStreamDestroy(c->cst);
 	if (c->t0) (void)hipEventDestroy(c->t0);
 	if (c->t1) (void)hipEventDestroy(c->t1);
 	if (c->ev_in) (void)hipEventDestroy(c->ev_in);
@@ -1165,8 +1170,12 @@ double wall_now()
 #ifndef VC_PIECE_BYTES
 #define VC_PIECE_BYTES ((uint64_t)16 << 20)
 #endif
+#ifndef VC_PIECE_BYTES_WARM
+#define VC_PIECE_BYTES_WARM ((uint64_t)32 << 20)
+#endif
 
-static int ingest_slot_alloc(Slot &s);
+static int ingest_slot_alloc(Slot &s, uint64_t piece);
+static size_t ingest_slot_bytes(uint64_t piece);
 
 namespace {
 
@@ -1174,7 +1183,7 @@ namespace {
 // pieces of a file go round robin over the shards.
 class DeviceSink : public VcIngestSink {
 public:
-	explicit DeviceSink(vc_ctx *c) : c_(c), n_(n_shards(c)) {}
+	DeviceSink(vc_ctx *c, uint64_t piece) : c_(c), n_(n_shards(c)), piece_(piece) {}
 	int acquire(int slot, VcSlotBuf *b) override
 	{
 		vc_ctx *sh;
@@ -1184,8 +1193,10 @@ public:
 			HIPCK(hipEventSynchronize(s.done));
 			s.pending = false;
 		}
-		if (!s.h_seq) {   // first use of the slot (reserve_ingest_slots, alloc = false)
-			const int rc = ingest_slot_alloc(s);
+		// first use of the slot (reserve_ingest_slots, alloc = false), or
+		// buffers sized for smaller pieces than this pass's
+		if (!s.h_seq || s.cap_bytes < ingest_slot_bytes(piece_)) {
+			const int rc = ingest_slot_alloc(s, piece_);
 			if (rc != VC_OK) return rc;
 		}
 		fill(s, b);
@@ -1216,14 +1227,23 @@ public:
 		fill(s, b);
 		return VC_OK;
 	}
+	// The copies go on the shard's copy stream and the kernels on its own
+	// stream, ordered by one event per slot: the DMA engine streams the pieces
+	// back to back instead of waiting for each piece's kernel.  A slot's next
+	// copy comes after the worker has waited for its `done` (the kernel that
+	// read its device buffers).
 	int submit(int slot, const VcSlotBuf &, uint64_t n, uint64_t bytes) override
 	{
 		vc_ctx *sh;
 		Slot &s = at(slot, &sh);
 		HIPCK(hipSetDevice(sh->dev));
-		HIPCK(hipMemcpyAsync(s.d_seq, s.h_seq, bytes, hipMemcpyHostToDevice, sh->st));
-		HIPCK(hipMemcpyAsync(s.d_offs, s.h_offs, n * sizeof(uint64_t), hipMemcpyHostToDevice, sh->st));
-		HIPCK(hipMemcpyAsync(s.d_lens, s.h_lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, sh->st));
+		if (!sh->cst) HIPCK(hipStreamCreateWithFlags(&sh->cst, hipStreamNonBlocking));
+		if (!s.copied) HIPCK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
+		HIPCK(hipMemcpyAsync(s.d_seq, s.h_seq, bytes, hipMemcpyHostToDevice, sh->cst));
+		HIPCK(hipMemcpyAsync(s.d_offs, s.h_offs, n * sizeof(uint64_t), hipMemcpyHostToDevice, sh->cst));
+		HIPCK(hipMemcpyAsync(s.d_lens, s.h_lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, sh->cst));
+		HIPCK(hipEventRecord(s.copied, sh->cst));
+		HIPCK(hipStreamWaitEvent(sh->st, s.copied, 0));
 		int rc = launch(sh, s.d_seq, bytes, s.d_offs, s.d_lens, n, sh->st, any_long(s.h_lens, n));
 		if (rc != VC_OK) return rc;
 		HIPCK(hipEventRecord(s.done, sh->st));
@@ -1235,6 +1255,7 @@ public:
 private:
 	vc_ctx *c_;
 	int n_;
+	uint64_t piece_;
 	Slot &at(int slot, vc_ctx **sh)
 	{
 		*sh = shard_at(c_, slot % n_);
@@ -1285,9 +1306,10 @@ static int reserve_ingest(vc_ctx *c, int threads, bool alloc)
 
 // One slot's buffers.  FASTQ: at most half of a piece's records' text is
 // sequence (the quality line is as long); FASTA and long records grow the slot.
-static int ingest_slot_alloc(Slot &s)
+static size_t ingest_slot_bytes(uint64_t piece) { return (size_t)piece / 2 + ((size_t)256 << 10); }
+static int ingest_slot_alloc(Slot &s, uint64_t piece)
 {
-	return slot_reserve(s, VC_PIECE_BYTES / 2 + ((size_t)256 << 10), VC_PIECE_BYTES / 256 + 4096);
+	return slot_reserve(s, ingest_slot_bytes(piece), (size_t)piece / 256 + 4096);
 }
 
 // alloc = false: only the slot records and their events; each slot's buffers
@@ -1305,7 +1327,7 @@ static int reserve_ingest_slots(vc_ctx *c, size_t slots, bool alloc)
 	for (size_t i = 0; alloc && i < slots; ++i) {
 		Slot &s = c->islot[i];
 		if (s.h_seq) continue;
-		int rc = ingest_slot_alloc(s);
+		int rc = ingest_slot_alloc(s, VC_PIECE_BYTES);
 		if (rc != VC_OK) return rc;
 	}
 	return VC_OK;
@@ -1324,10 +1346,19 @@ static int count_file_parallel(vc_ctx *c, int fd, uint64_t size, int block_bases
 	const int threads = clamp_threads(n_threads);
 	const int slots = reserve_ingest(c, threads, false);
 	if (slots < 0) return slots;
-	DeviceSink sink(c);
+	// pieces of 16 MB while the counter's slots are first pinned (the pinning
+	// is paid inside the pass, by the workers); once a pass has pinned them,
+	// later passes and files use 32 MB pieces (the slots grow once): half the
+	// copies, kernels and events per byte (profiles/r05i_*: 39.7-40.5 against
+	// 35.5-36.1 Gbases/s in one process; in a fresh CLI process the 32 MB
+	// slots' pinning made the pass 40 % slower, profiles/r05i_cli_piece_ab.json)
 	const char *pe = getenv("VAFC_INGEST_PIECE");          // test knob: piece size in bytes
-	const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : VC_PIECE_BYTES;
-	return vc_ingest_plain(fd, size, c->k, block_bases, threads, slots, piece, sink, st, range);
+	const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe)
+	                                            : (c->ingest_warm ? VC_PIECE_BYTES_WARM : VC_PIECE_BYTES);
+	DeviceSink sink(c, piece);
+	const int rc = vc_ingest_plain(fd, size, c->k, block_bases, threads, slots, piece, sink, st, range);
+	if (rc == VC_OK) c->ingest_warm = true;
+	return rc;
 }
 
 // gzip input: the text the parallel inflater produces (n_threads workers) is
@@ -1337,9 +1368,9 @@ static int count_file_gzip(vc_ctx *c, VcGzParallel *g, int block_bases, int n_th
 	const int parsers = vc_gz_parse_threads(clamp_threads(n_threads));
 	const int slots = reserve_ingest(c, parsers, false);
 	if (slots < 0) return slots;
-	DeviceSink sink(c);
 	const char *pe = getenv("VAFC_INGEST_PIECE");          // test knob: piece size in bytes
 	const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : VC_PIECE_BYTES;
+	DeviceSink sink(c, piece);
 	return vc_ingest_gzip(g, c->k, block_bases, parsers, slots, piece, (uint64_t)(slots + 2) * piece * 2, sink, st);
 }
 
@@ -1419,16 +1450,19 @@ extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n
 	vc_file_stats local = {0, 0, 0, 0.0};
 	const double t0 = wall_now();
 	HIPCK(hipSetDevice(c->dev));
-	// the reader threads spawned below run on the GPU's NUMA node
-	VcAffinityScope placement(gpu_cpus(c, clamp_threads(n_threads)));
+	const int fd = open(path, O_RDONLY);
+	if (fd < 0) return VC_EIO;
+	struct stat sb;
+	uint8_t magic[2] = {0, 0};
+	const bool reg = fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
+	const bool gz = reg && pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+	const bool plain = reg && !gz;
+	// the reader threads spawned below run on the GPU's NUMA node when it has
+	// a CPU for each of them: the parse workers, or for gzip the inflaters,
+	// the parsers of the inflated text, the pump and the block loop
+	const int t = clamp_threads(n_threads);
+	VcAffinityScope placement(gpu_cpus(c, gz ? vc_gz_inflate_threads(t) + vc_gz_parse_threads(t) + 2 : t));
 	{
-		const int fd = open(path, O_RDONLY);
-		if (fd < 0) return VC_EIO;
-		struct stat sb;
-		uint8_t magic[2] = {0, 0};
-		const bool reg = fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
-		const bool gz = reg && pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
-		const bool plain = reg && !gz;
 		const char *me = getenv("VAFC_INGEST_MIN");        // test knob: smallest file for the parallel reader
 		const uint64_t min_bytes = me ? (uint64_t)atoll(me) : VC_PARALLEL_MIN_BYTES;
 		if (plain && (uint64_t)sb.st_size >= min_bytes && sb.st_size > 0) {

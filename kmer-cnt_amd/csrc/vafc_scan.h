@@ -335,15 +335,43 @@ __device__ __forceinline__ uint64_t vc_canon_from_strands(uint32_t flo, uint32_t
 	return f < r ? f : r;
 }
 
-// Large-panel kernels with VC_BIG_SYMQ: entries are (rlo << 32) | flo and the
-// second-level filter is keyed by the strands (vc_l2s_*); only survivors
-// rebuild the canonical k-mer and hash it for the exact table.
-template <int ABL>
-__device__ __forceinline__ void drain_range_sym(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
-                                                uint32_t hi, int lane)
+#ifdef VC_BIG_RAWQ   // A/B: the large-panel kernels queue forward k-mers like the others (round 4)
+#define VC_SYMQ(ABL) false
+#else
+#define VC_SYMQ(ABL) (((ABL) & VC_KV_BIG) != 0)
+#endif
+#ifdef VC_BIG_DRAIN_ALL
+#define VC_DRAIN_ALL 1
+#else
+#define VC_DRAIN_ALL 0
+#endif
+#ifdef VC_NO_DEFER_PROBE   // A/B: near-full drains probe their survivors at once (round 4)
+#define VC_DEFER_PROBE 0
+#else
+#define VC_DEFER_PROBE 1
+#endif
+
+// Large-panel kernels (VC_SYMQ): the second-level filter is keyed by the two
+// strands' low words (vc_l2s_*).  The queue holds the forward k-mer as every
+// kernel queues it; the drain takes flo = its low word and rlo = the reverse
+// complement of its first sixteen bases (one v_alignbit at a run-time shift
+// and a 16-base reverse complement), with no 64-bit reverse complement,
+// canonical minimum or 64-bit hash; only survivors rebuild the canonical
+// k-mer (vc_canon_from_strands) and hash it for the exact table.
+// A near-full drain (KEEP) does not probe its survivors: it writes them back
+// at the bottom of the drained range and returns how many, so that they wait
+// in the queue for the read group's final drain, where one probe latency
+// covers them all, instead of costing this drain a dependent table load.
+// When more survive than `room` entries (a read set dense in keys), they are
+// probed at once.  The final drain (KEEP = false) probes every survivor.
+template <int ABL, bool KEEP>
+__device__ __forceinline__ uint32_t drain_range_sym(const VcKernelArgs &A, uint64_t *q, uint32_t lo,
+                                                    uint32_t hi, int lane, uint32_t room)
 {
 	uint32_t fl[4], rl[4], w[4], m[4];
+	uint64_t e64[4];
 	const uint32_t l2sh = 32u - A.l2bits;
+	const uint32_t fsh16 = 2u * (uint32_t)(A.k - 16);   // the window's first sixteen bases
 #pragma unroll
 	for (int r = 0; r < 4; ++r) {
 		const uint32_t i = lo + (uint32_t)(r * WAVE + lane);
@@ -352,45 +380,68 @@ __device__ __forceinline__ void drain_range_sym(const VcKernelArgs &A, const uin
 		m[r] = 1;
 		if (i < hi) {
 			const uint64_t e = q[i];
+			e64[r] = e;
 			fl[r] = (uint32_t)e;
-			rl[r] = (uint32_t)(e >> 32);
+			rl[r] = rc16(__builtin_amdgcn_alignbit((uint32_t)(e >> 32), (uint32_t)e, fsh16));
 			const uint32_t hw = vc_l2s_hash(fl[r], rl[r]);
 			m[r] = vc_l2f_mask(vc_l2s_hash2(fl[r], rl[r]));
 			if constexpr ((ABL & VC_ABL_NOGATHER) != 0) asm volatile("" :: "v"(hw >> l2sh), "v"(m[r]));
 			else w[r] = A.l2f[hw >> l2sh];
 		}
 	}
-	if constexpr ((ABL & VC_ABL_NOGATHER) != 0) return;
+	if constexpr ((ABL & VC_ABL_NOGATHER) != 0) return 0;
+	bool surv[4];
+#pragma unroll
+	for (int r = 0; r < 4; ++r) surv[r] = (w[r] & m[r]) == m[r];   // false for empty entries (w = 0, m = 1)
+	if constexpr (KEEP && VC_DEFER_PROBE) {
+		uint64_t bal[4];
+		uint32_t n = 0;
+#pragma unroll
+		for (int r = 0; r < 4; ++r) {
+			bal[r] = __ballot(surv[r]);
+			n += (uint32_t)__popcll(bal[r]);
+		}
+		if (n == 0) return 0;
+		if (n <= room) {
+			uint32_t at = lo;
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[r] >> 32),
+				                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal[r], 0u));
+				if (surv[r]) q[at + pre] = e64[r];
+				at += (uint32_t)__popcll(bal[r]);
+			}
+			return n;
+		}
+	}
 #pragma unroll
 	for (int r = 0; r < 4; ++r) {
-		if ((w[r] & m[r]) != m[r]) continue;      // also skips empty entries (w = 0, m = 1)
+		if (!surv[r]) continue;
 		const uint64_t key = vc_canon_from_strands(fl[r], rl[r], A.k);
 		probe_key<ABL>(A, key, vc_hash(key));
 	}
+	return 0;
 }
 
-#ifdef VC_BIG_SYMQ
-#define VC_SYMQ(ABL) (((ABL) & VC_KV_BIG) != 0)
-#else
-#define VC_SYMQ(ABL) false
-#endif
-
-template <int ABL>
-__device__ __forceinline__ void drain_range(const VcKernelArgs &A, const uint64_t *q, uint32_t lo,
-                                            uint32_t hi, int lane)
+// Drain queue entries [lo, hi).  KEEP (near-full drains of the large-panel
+// kernels): survivors of the second-level filter may be kept at q[lo ..
+// lo + returned) for a later drain, at most `room` of them; otherwise every
+// entry is resolved and 0 is returned.
+template <int ABL, bool KEEP = false>
+__device__ __forceinline__ uint32_t drain_range(const VcKernelArgs &A, uint64_t *q, uint32_t lo,
+                                                uint32_t hi, int lane, uint32_t room = 0)
 {
 	__builtin_amdgcn_wave_barrier();
 	if constexpr ((ABL & VC_ABL_NODRAIN) != 0) {
 		asm volatile("" :: "v"(q[lo + (uint32_t)lane]));
-		return;
+		return 0;
 	}
 	if constexpr (VC_SYMQ(ABL)) {
-		drain_range_sym<ABL>(A, q, lo, hi, lane);
-		return;
+		return drain_range_sym<ABL, KEEP>(A, q, lo, hi, lane, room);
 	}
 	if (A.l2bits) {
 		drain_range_l2f<ABL>(A, q, lo, hi, lane);
-		return;
+		return 0;
 	}
 	uint64_t key[4];
 	uint32_t s[4];
@@ -424,6 +475,7 @@ __device__ __forceinline__ void drain_range(const VcKernelArgs &A, const uint64_
 			x = *reinterpret_cast<const uint4 *>(&A.table[t]);
 		}
 	}
+	return 0;
 }
 
 // Lanes with `hit` append `key` (bal = ballot(hit) != 0).  The queue is
@@ -438,8 +490,10 @@ __device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q
 	if (hit) Q.q[Q.n + pre] = key;
 	Q.n = __builtin_amdgcn_readfirstlane(Q.n + (uint32_t)__popcll(bal));
 	if (Q.n > A.qcap - WAVE) {        // A.qcap >= 2 WAVE
-		drain_range<ABL>(A, Q.q, Q.n - WAVE, Q.n, lane);
-		Q.n -= WAVE;
+		// kept survivors must leave room for one more full append (<= WAVE);
+		// VC_BIG_DRAIN_ALL (A/B): the large-panel kernels drain the whole queue
+		const uint32_t lo = (VC_SYMQ(ABL) && VC_DRAIN_ALL) ? 0u : Q.n - WAVE;
+		Q.n = lo + drain_range<ABL, true>(A, Q.q, lo, Q.n, lane, A.qcap - WAVE - lo);
 		// leave nothing in flight on this (rare) path, so that the compiler
 		// can keep counting the scan's prefetches across it
 		__builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
@@ -966,18 +1020,8 @@ __device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, i
 			// lowest pass first; lanes without one compute a garbage key they do not append
 			const uint32_t b = (uint32_t)__builtin_ctz(hm | 0x80000000u);   // hm < 2^16
 			const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, 2u * b);
-			if constexpr (VC_SYMQ(ABL)) {
-				// the reverse strand's low word: the C stream from the window's
-				// first base, s2 = 48 - K - b bases into chunk c - 2 (2 <= s2 <= 27
-				// for K >= 21); v_alignbit takes the shift modulo 32
-				const uint32_t s2 = (uint32_t)(48 - K) - b;
-				const bool up = s2 >= 16u;
-				const uint32_t rlo = __builtin_amdgcn_alignbit(up ? Cc : Cm1, up ? Cm1 : Cm2, 2u * s2);
-				queue_append<ABL>(A, Q, bal, has, ((uint64_t)rlo << 32) | flo, lane);
-			} else {
-				const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
-				queue_append<ABL>(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
-			}
+			const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
+			queue_append<ABL>(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
 			hm &= hm - 1u;
 		}
 	}
@@ -998,8 +1042,6 @@ __device__ __forceinline__ void hit_loop2(const VcKernelArgs &A, WaveQueue &Q, u
                                           uint32_t Bam1, uint32_t Ba, uint32_t Bb, int lane)
 {
 	constexpr uint32_t HIM = (1u << (2 * K - 32)) - 1u;
-	static_assert(!(VC_SYMQ(ABL) && VC_KV_BIG_DEFER != 0),
-	              "hit_loop2 queues forward k-mers (VC_DEFER_BIG and VC_BIG_SYMQ exclude each other)");
 	if constexpr ((ABL & 4) != 0) {
 		asm volatile("" :: "v"(hm));
 	} else if (__ballot(hm != 0u)) {
