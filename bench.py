@@ -91,16 +91,17 @@ LIMITER_FLANK = ("the roofline is HBM (integer byte work, no MFMA); the kernel r
                  "the flank lookups); an ablation in one process puts 85 % of the time in instruction issue "
                  "(VALU-only variant 4.19 of 4.93 ms), 10 % in the hit path, 4 % in the read loads and 0.6 % in "
                  "the LDS lookups (their bank conflicts, 0.70 of the LDS cycles, hide behind the other waves); "
-                 "HBM requests are 1.47x the algorithmic bytes (the waves' live read lines, 4.9 MB per XCD, "
+                 "HBM requests are 1.48x the algorithmic bytes (the waves' live read lines, 4.9 MB per XCD, "
                  "overflow its 4 MB L2 and are fetched again), not the limit; DESIGN.md sections 3.1.1-3.1.2, "
-                 "profiles/r04j_final_c2_pmc_counters.json, profiles/r04c_ablation_time.log")
+                 "profiles/r05final_c2_pmc_counters.json, profiles/r04c_ablation_time.log")
 LIMITER_LARGE_PANEL = ("the roofline is HBM (integer byte work, no MFMA); the large-panel kernel runs far below "
-                       "it, bound by VALU issue and the texture-address (TA) rate of its gathers: 9.3 % of "
-                       "windows pass the 144 KiB LDS Bloom filter (about 6 % is that size's information limit "
-                       "for 200k SNP pairs), each pass is a hit-loop trip and one lane of a random gather into "
-                       "the L2-resident second-level filter; 23.6 VALU per base (5.5 G per launch, ~0.8 of the "
-                       "kernel time at ~4 cycles each), TA busy ~0.5 of the cycles (3.66 G over 256 CUs); "
-                       "DESIGN.md section 3.1 (large panels), profiles/r04j_final_c5_pmc_counters.json")
+                       "it, bound by VALU issue and the L1 tag rate of its gathers: 9.3 % of windows pass the "
+                       "144 KiB LDS Bloom filter (about 6 % is that size's information limit for 200k SNP pairs); "
+                       "an ablation puts 57 % of the time in the scan (Bloom lookups at 9 VALU a window), 15 % in "
+                       "the hit loop, 10 % in the drains' arithmetic, 15 % in the gathers into the L2-resident "
+                       "second-level filter (64 distinct lines per instruction) and 3 % in the exact-table probes; "
+                       "23.1 VALU per base (5.41 G per launch), TA busy 3.61 G cycles over 256 CUs; DESIGN.md "
+                       "section 3.1.3, profiles/r05final_c5_pmc_counters.json, profiles/r05l_abl_time.log")
 
 
 def cli_run(binary, pat, fq, threads, out, k, env=None, timeout=900):
@@ -440,6 +441,8 @@ def rank_threads(world):
     """Reader threads per rank: the CPU share of one GPU (16 on the GPU pool),
     no more than the affinity mask or the cgroup's CPU quota split over the
     ranks on this node."""
+    if os.environ.get("VAFC_BENCH_THREADS"):      # experiments: a fixed count per rank
+        return max(1, int(os.environ["VAFC_BENCH_THREADS"]))
     n = cpu_share(1)
     try:
         aff = len(os.sched_getaffinity(0))
@@ -638,6 +641,12 @@ def main():
     if args.config == "c5":
         args.panel = "syn200k"
 
+    # stdout carries the one JSON line only: everything else a rank's
+    # libraries print there (gloo's "[Gloo] Rank 0 is connected ..." lines)
+    # goes to stderr, the line to the saved descriptor
+    out_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
     # one GPU per rank; the modulo only matters for rehearsals with more ranks
@@ -941,7 +950,7 @@ def main():
             "e2e": e2e,
             "cli": cli,
         }
-        print(json.dumps(line), flush=True)
+        os.write(out_fd, (json.dumps(line) + "\n").encode())
     kmap.close()
     shutil.rmtree(tmp, ignore_errors=True)
     if world > 1:
