@@ -52,7 +52,10 @@ ssize_t pread_full(int fd, uint8_t *p, size_t n, uint64_t off)
 // (VcTextSource::view): no copy, but on the box's tmpfs-cached C2 stream the
 // page faults of 16 threads cost more than the copies they save -- the
 // reader alone 34 against 57 GB/s of text, the CLI 12.7 against 20.5
-// Gbases/s (profiles/r04g_mmap_ab.json).
+// Gbases/s (profiles/r04g_mmap_ab.json).  Populating
+// each piece's page table entries with one madvise(MADV_POPULATE_READ)
+// before parsing it was worse still in round 5: 14.6 against 39.2 Gbases/s
+// (profiles/r05m1_mmap_populate_bench.json).
 class FdSource : public VcIngestSource {
 public:
 	FdSource(int fd, uint64_t size) : fd_(fd), size_(size)
