@@ -340,6 +340,15 @@ __device__ __forceinline__ uint64_t vc_canon_from_strands(uint32_t flo, uint32_t
 #else
 #define VC_SYMQ(ABL) (((ABL) & VC_KV_BIG) != 0)
 #endif
+// The hit loops queue the forward k-mer's high word unmasked (bits above 2k
+// hold older bases): every drain masks the entry with A.kmask, and the
+// large-panel drain reads only bits below 2k (the low word and bits
+// 2(k - 16) .. 2k of the entry).  -DVC_HIT_MASK (A/B) masks it in the loop.
+#ifdef VC_HIT_MASK
+#define VC_HIT_HIM HIM
+#else
+#define VC_HIT_HIM (HIM | ~0u)
+#endif
 #ifdef VC_BIG_DRAIN_ALL
 #define VC_DRAIN_ALL 1
 #else
@@ -908,9 +917,11 @@ __device__ __forceinline__ uint32_t bloom_bits_big(const VcKernelArgs &A, uint32
 		const uint32_t f20 = __builtin_amdgcn_ubfe(bsrc, (uint32_t)(2 * (bo + 15 - j)), 20u);
 		const int co = plan.co[j];
 		const uint32_t r20 = __builtin_amdgcn_ubfe(c_reg(co, Cm2, Cm1, Cc), (uint32_t)(2 * (j - K + 1 - co)), 20u);
+		// the filter sits at LDS address 0 (checked at kernel entry): a plain
+		// v_and_b32 makes the word address, not a v_and_or_b32 with fbase
 		const uint32_t a = __umulhi(f20 * r20, nw4) & ~3u;
 		if constexpr ((ABL & 1) != 0) { asm volatile("" :: "v"(a)); fw[j] = a; }
-		else fw[j] = *(lds_u32_t *)(uintptr_t)(a | fbase);
+		else fw[j] = *(lds_u32_t *)(uintptr_t)a;
 		fl[j] = f20;
 		rl[j] = r20;
 	}
@@ -919,6 +930,47 @@ __device__ __forceinline__ uint32_t bloom_bits_big(const VcKernelArgs &A, uint32
 	for (int j = J0; j < J1; ++j) hm = (hm << 1) | ((fw[j] >> (fl[j] & 31u)) & (fw[j] >> (rl[j] & 31u)) & 1u);
 	if constexpr (J1 < 16) hm <<= 16 - J1;
 	return hm;
+}
+
+// A chunk's filter lookups issued VC_BIG_GROUP / VC_FLANK_GROUP windows at a
+// time, each group's bits tested before the next group's lookups issue (an
+// empty asm with a memory clobber keeps the compiler from hoisting them): the
+// live ranges of the looked-up words and their operands shrink (C5 kernel 124
+// -> 112 VGPRs), and the compiler no longer re-derives the bit positions it
+// could not keep in registers.  The lookup latency is covered by the other
+// three waves of the SIMD.  C5 10.69-10.73 -> 10.58-10.62 ms with the plain
+// address mask above (profiles/r05o_ab.log, r05p_ab.log; groups of 4 the same);
+// the flank kernel's lookups in groups of 8 or 4 were not faster (r05q_ab.log).
+#ifndef VC_BIG_GROUP
+#define VC_BIG_GROUP 8
+#endif
+#ifndef VC_FLANK_GROUP
+#define VC_FLANK_GROUP 16
+#endif
+template <int K, int J0, int J1, int ABL>
+__device__ __forceinline__ uint32_t bloom_bits_big_grouped(const VcKernelArgs &A, uint32_t fbase, uint32_t Bm1, uint32_t Bc,
+                                                          uint32_t Cm2, uint32_t Cm1, uint32_t Cc)
+{
+	if constexpr (J1 - J0 <= VC_BIG_GROUP) {
+		return bloom_bits_big<K, J0, J1, ABL>(A, fbase, Bm1, Bc, Cm2, Cm1, Cc);
+	} else {
+		constexpr int JM = J0 + VC_BIG_GROUP;
+		uint32_t h = bloom_bits_big<K, J0, JM, ABL>(A, fbase, Bm1, Bc, Cm2, Cm1, Cc);
+		asm volatile("" : "+v"(h) :: "memory");
+		return h | bloom_bits_big_grouped<K, JM, J1, ABL>(A, fbase, Bm1, Bc, Cm2, Cm1, Cc);
+	}
+}
+template <int J0, int J1, int ABL>
+__device__ __forceinline__ uint32_t flank_bits_u8_grouped(uint32_t Bm1, uint32_t Bc)
+{
+	if constexpr (J1 - J0 <= VC_FLANK_GROUP) {
+		return flank_bits_u8<J0, J1, ABL>(Bm1, Bc);
+	} else {
+		constexpr int JM = J0 + VC_FLANK_GROUP;
+		uint32_t h = flank_bits_u8<J0, JM, ABL>(Bm1, Bc);
+		asm volatile("" : "+v"(h) :: "memory");
+		return h | flank_bits_u8_grouped<JM, J1, ABL>(Bm1, Bc);
+	}
 }
 
 // One 16-base chunk c of the packed scan from its five dwords (w0: the dword
@@ -954,14 +1006,14 @@ __device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, i
 		// there; window j passes iff the 10-mers ending at j (its last ten
 		// bases) and at j - (K - 10) (its first ten) are both in the set
 		(void)fsh; (void)wmask4; (void)Cm2;
-		if constexpr (VC_FLANK_U8) hm = flank_bits_u8<J0, J1, ABL>(Bm1, Bc);
+		if constexpr (VC_FLANK_U8) hm = flank_bits_u8_grouped<J0, J1, ABL>(Bm1, Bc);
 		else hm = flank_bits<J0, J1, ABL>(fbase, Bm1, Bc);
 		const uint32_t P = (H << 16) | hm;           // R of chunks c-1 | c, c-2 in H >> 16
 		hm = flank_windows<K>(hm, H, P);
 		H = P;
 	} else if constexpr ((ABL & VC_KV_BIG) != 0) {
 		(void)fsh; (void)wmask4;
-		hm = bloom_bits_big<K, J0, J1, ABL>(A, fbase, Bm1, Bc, Cm2, Cm1, Cc);
+		hm = bloom_bits_big_grouped<K, J0, J1, ABL>(A, fbase, Bm1, Bc, Cm2, Cm1, Cc);
 	} else {
 	// pass <=> bits (flo & 31) and (rlo & 31) of the filter word are set:
 	// hm = (hm << 1) | ((w >> flo) & (w >> rlo) & 1), 4 VALU per window
@@ -1020,7 +1072,7 @@ __device__ __forceinline__ uint32_t packed_chunk(const VcKernelArgs &A, int c, i
 			// lowest pass first; lanes without one compute a garbage key they do not append
 			const uint32_t b = (uint32_t)__builtin_ctz(hm | 0x80000000u);   // hm < 2^16
 			const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, 2u * b);
-			const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
+			const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & VC_HIT_HIM;
 			queue_append<ABL>(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
 			hm &= hm - 1u;
 		}
@@ -1054,7 +1106,7 @@ __device__ __forceinline__ void hit_loop2(const VcKernelArgs &A, WaveQueue &Q, u
 			const bool ina = b >= 16u;
 			const uint32_t lo = ina ? Ba : Bb, hi = ina ? Bam1 : Ba, hi2 = ina ? Bam2 : Bam1;
 			const uint32_t flo = __builtin_amdgcn_alignbit(hi, lo, 2u * b);
-			const uint32_t fhi = __builtin_amdgcn_alignbit(hi2, hi, 2u * b) & HIM;
+			const uint32_t fhi = __builtin_amdgcn_alignbit(hi2, hi, 2u * b) & VC_HIT_HIM;
 			queue_append<ABL>(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
 			hm &= hm - 1u;
 		}
@@ -1519,7 +1571,7 @@ __device__ __forceinline__ uint32_t packed_chunk_fb(const VcKernelArgs &A, const
 	Qe += 16;
 	const uint32_t Bc = pack_fb(D, t0, t1, t2, t3);
 	uint32_t hm;
-	if constexpr (VC_FLANK_U8) hm = flank_bits_u8<J0, J1, ABL>(Bm1, Bc);
+	if constexpr (VC_FLANK_U8) hm = flank_bits_u8_grouped<J0, J1, ABL>(Bm1, Bc);
 	else hm = flank_bits<J0, J1, ABL>(lds_base(filt), Bm1, Bc);
 	const uint32_t P = (H << 16) | hm;
 	hm = flank_windows<K>(hm, H, P);
@@ -1550,7 +1602,7 @@ __device__ __forceinline__ uint32_t packed_chunk_fb(const VcKernelArgs &A, const
 			if (!bal) break;
 			const uint32_t b = (uint32_t)__builtin_ctz(hm | 0x80000000u);
 			const uint32_t flo = __builtin_amdgcn_alignbit(Bm1, Bc, 2u * b);
-			const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & HIM;
+			const uint32_t fhi = __builtin_amdgcn_alignbit(Bm2, Bm1, 2u * b) & VC_HIT_HIM;
 			queue_append<ABL>(A, Q, bal, has, ((uint64_t)fhi << 32) | flo, lane);
 			hm &= hm - 1u;
 		}

@@ -366,6 +366,51 @@ def test_count_file_equals_oracle_file_pass(tmp_path):
     assert np.array_equal(got, want[: 2 * orc.n_patterns])
 
 
+@pytest.mark.parametrize("world,piece", [(3, 1 << 20), (5, 4_000_037), (2, 0)])
+def test_count_file_ranges_chain_to_whole_file(world, piece, tmp_path, monkeypatch):
+    """vc_count_file_range over a 120k-read FASTQ (~45 MB) cut into `world`
+    byte ranges the way vafc_dist.byte_range cuts it (cuts fall inside
+    records), every range counted into ONE map on the device, many reader
+    pieces per range (piece 0: the default size): the ranges chain (each
+    begins where the previous one ended, no truncated record), their bases and
+    reads add up to the oracle's whole-file pass, and the counts and k-mer
+    tally equal it bit for bit."""
+    import vafc
+    import vafc_dist as D
+    import vafc_synth as S
+    import oracle as O
+    panel = S.grch38_panel()
+    pat = str(tmp_path / "p.txt")
+    panel.write_patterns(pat, 21)
+    fq = str(tmp_path / "r.fq")
+    S.write_fastq(fq, panel, 120_000, seed=11 + world, f_snp=0.2)
+    size = os.path.getsize(fq)
+    monkeypatch.setenv("VAFC_INGEST_MIN", "0")
+    if piece:
+        monkeypatch.setenv("VAFC_INGEST_PIECE", str(piece))
+    db = vafc.load_patterns(pat)
+    m = vafc.create_combined_kmer_map(db, 21)
+    infos, bases, seqs = [], 0, 0
+    for r in range(world):
+        b, e = D.byte_range(size, r, world)
+        st, ri = m.count_file_range(fq, b, e, 10_000_000, 4)
+        assert ri.whole == 0 and ri.errs == 0 and ri.stopped == (r == world - 1)
+        infos.append((ri.first, ri.next, ri.errs, ri.stopped))
+        bases += st.bases
+        seqs += st.seqs
+    assert D.chain_holds(infos), infos
+    assert infos[-1][1] == D.NO_OFFSET
+    got, km = m.finish()
+    m.close()
+    orc = O.Oracle(21, pattern_fn=pat)
+    want = np.zeros(2 * orc.n_patterns + 2, np.uint32)
+    rc, wb, ws, km_want = orc.count_file(fq, 10_000_000, want)
+    assert rc == 0 and (bases, seqs) == (wb, ws) == (bases, 120_000)
+    assert km == km_want
+    assert np.array_equal(got, want[: 2 * orc.n_patterns])
+    assert int(got.sum()) > 0
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_count_file_parallel_reader_on_fuzzed_input(seed, tmp_path, monkeypatch):
     """vc_count_file's parallel reader (forced onto a small file with tiny

@@ -38,6 +38,32 @@ def word_big(fl, rl, nwords):
     return ((p * np.uint64(nwords)) >> np.uint64(32)).astype(np.int64)
 
 
+def fp_unaligned(keys, q, nwords):
+    """The 32 bits at byte offset (p * (4 nwords - 3)) >> 32 of the filter,
+    any alignment (no address mask in the kernel).  Tried in round 5: fewer
+    false positives, but unaligned LDS dword reads made the C5 kernel 2.15x
+    slower (profiles/r05n_ab_unaligned_lds.log), so not kept."""
+    nb = 4 * nwords
+    F = np.zeros(nb + 8, np.uint8)
+
+    def off(fl, rl):
+        p = ((fl.astype(np.uint64) & M20) * (rl.astype(np.uint64) & M20)) & M32
+        return ((p * np.uint64(nb - 3)) >> np.uint64(32)).astype(np.int64)
+
+    fl, rl = strands(keys)
+    b = off(fl, rl)
+    for s in (fl, rl):
+        g = 8 * b + (s & np.uint32(31)).astype(np.int64)
+        np.bitwise_or.at(F, g >> 3, (np.uint8(1) << (g & 7).astype(np.uint8)))
+    qf, qr = strands(q)
+    qb = off(qf, qr)
+    ok = np.ones(len(q), bool)
+    for s in (qf, qr):
+        g = 8 * qb + (s & np.uint32(31)).astype(np.int64)
+        ok &= ((F[g >> 3] >> (g & 7).astype(np.uint8)) & 1) == 1
+    return float(np.mean(ok))
+
+
 def fp(keys, q, word, nwords):
     F = np.zeros(nwords, np.uint32)
     fl, rl = strands(keys)
@@ -61,6 +87,7 @@ def main():
     print("128 KiB, power of two (vc_filter_word):  FP %.4f" % fp(keys, q, word_pow2, 32768))
     for kib_words in (32768, 34816, 36860):
         print("%6.2f KiB, multiply-high (vc_big_word): FP %.4f" % (kib_words / 256, fp(keys, q, word_big, kib_words)))
+    print("%6.2f KiB, any byte offset (not kept):     FP %.4f" % (36860 / 256, fp_unaligned(keys, q, 36860)))
 
 
 if __name__ == "__main__":
