@@ -192,11 +192,24 @@ __device__ __forceinline__ uint32_t ldw(const uint32_t *__restrict__ s32, uint64
 // when all four are inside the buffer, else four clamped dword loads (the
 // last reads of a batch).  Loaded bytes past a read's end are masked later.
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+// The read stream's 16-byte loads.  -DVC_NT_READS (A/B): non-temporal loads,
+// meant to keep the streamed reads from pushing the second-level filter out of
+// the L2 -- but a lane's consecutive chunk loads share cache lines, which the
+// non-temporal loads lose: C5 10.58 -> 12.19 ms, C2 4.91 -> 7.70 ms
+// (profiles/r05v_ab.log, r05w_ab.log).
+__device__ __forceinline__ u32x4a4 ld16(const uint32_t *__restrict__ p)
+{
+#ifdef VC_NT_READS
+	return __builtin_nontemporal_load(reinterpret_cast<const u32x4a4 *>(p));
+#else
+	return *reinterpret_cast<const u32x4a4 *>(p);
+#endif
+}
 __device__ __forceinline__ void ld4(const uint32_t *__restrict__ s32, uint64_t i, uint64_t wmax,
                                     uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
 {
 	if (i + 3 <= wmax) {
-		const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(s32 + i);
+		const u32x4a4 v = ld16(s32 + i);
 		a = v.x; b = v.y; c = v.z; d = v.w;
 	} else {
 		a = ldw(s32, i, wmax); b = ldw(s32, i + 1, wmax); c = ldw(s32, i + 2, wmax); d = ldw(s32, i + 3, wmax);
@@ -1167,7 +1180,7 @@ __device__ __forceinline__ uint32_t ldq(const uint32_t *__restrict__ s32, uint64
 {
 	const uint64_t lim = wmax - 3u;
 	const bool clamp = q > lim;
-	const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(s32 + (clamp ? lim : q));
+	const u32x4a4 v = ld16(s32 + (clamp ? lim : q));
 	a = v.x; b = v.y; c = v.z; d = v.w;
 	return clamp ? (q - lim > 3u ? 3u : (uint32_t)(q - lim)) : 0u;
 }
@@ -1179,7 +1192,7 @@ __device__ __forceinline__ uint32_t ldq_s(const uint32_t *__restrict__ s32, uint
                                           uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
 {
 	if constexpr (SAFE) {
-		const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(s32 + q);
+		const u32x4a4 v = ld16(s32 + q);
 		a = v.x; b = v.y; c = v.z; d = v.w;
 		return 0u;
 	} else {
@@ -1647,7 +1660,7 @@ __device__ __forceinline__ int ldq_fb(const uint32_t *__restrict__ s32, int64_t 
 {
 	const int64_t lim = (int64_t)wmax - 3;
 	const int64_t cq = q < 0 ? 0 : (q > lim ? lim : q);
-	const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(s32 + cq);
+	const u32x4a4 v = ld16(s32 + cq);
 	a = v.x; b = v.y; c = v.z; d = v.w;
 	const int64_t sft = q - cq;
 	return sft > 3 ? 3 : (sft < -3 ? -3 : (int)sft);
@@ -1658,7 +1671,7 @@ __device__ __forceinline__ int ldq_fb_s(const uint32_t *__restrict__ s32, int64_
                                         uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
 {
 	if constexpr (SAFE) {
-		const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(s32 + q);
+		const u32x4a4 v = ld16(s32 + q);
 		a = v.x; b = v.y; c = v.z; d = v.w;
 		return 0;
 	} else {
