@@ -132,18 +132,22 @@ VC_HD uint32_t vc_l2f_mask(uint32_t h2)
  * the canonical k-mer (vc_canon_from_strands).  Symmetric in (flo, rlo), so it is a
  * function of the canonical k-mer.  Word from the top bits of one mix, bits
  * from a second one. */
-VC_HD uint32_t vc_l2s_hash(uint32_t flo, uint32_t rlo)
+#define VC_L2S_M 0x9E3779B1u
+/* the two mixes of the strands' products u = flo * M, v = rlo * M */
+VC_HD uint32_t vc_l2s_mix1(uint32_t u, uint32_t v)
 {
-	uint32_t x = flo * 0x9E3779B1u + rlo * 0x9E3779B1u;
+	uint32_t x = u + v;
 	x ^= x >> 15;
 	return x * 0x85EBCA77u;
 }
-VC_HD uint32_t vc_l2s_hash2(uint32_t flo, uint32_t rlo)
+VC_HD uint32_t vc_l2s_mix2(uint32_t u, uint32_t v)
 {
-	uint32_t y = (flo * 0x9E3779B1u) ^ (rlo * 0x9E3779B1u);
+	uint32_t y = u ^ v;
 	y ^= y >> 13;
 	return y * 0xC2B2AE3Du;
 }
+VC_HD uint32_t vc_l2s_hash(uint32_t flo, uint32_t rlo) { return vc_l2s_mix1(flo * VC_L2S_M, rlo * VC_L2S_M); }
+VC_HD uint32_t vc_l2s_hash2(uint32_t flo, uint32_t rlo) { return vc_l2s_mix2(flo * VC_L2S_M, rlo * VC_L2S_M); }
 
 /* Large panels (a second-level filter in use) and k >= 21: a larger LDS
  * Bloom filter, VC_BIG_FILTER_WORDS 32-bit words (144 KiB: the queues shrink

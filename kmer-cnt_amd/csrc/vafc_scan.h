@@ -338,7 +338,10 @@ __device__ __forceinline__ void drain_range_l2f(const VcKernelArgs &A, const uin
 __device__ __forceinline__ uint32_t rc16(uint32_t x)
 {
 	x = __builtin_bitreverse32(x);
-	return ~(((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1));
+	// swap the bits of each pair and complement: ~(M ? x >> 1 : x << 1),
+	// M = 0x55555555, in one v_bitop3 (table 0x1B); the compiler's own form
+	// spent a v_and on x << 1 first
+	return __builtin_amdgcn_bitop3_b32(x >> 1, x << 1, 0x55555555u, 0x1B);
 }
 __device__ __forceinline__ uint64_t vc_canon_from_strands(uint32_t flo, uint32_t rlo, int k)
 {
@@ -390,23 +393,34 @@ template <int ABL, bool KEEP>
 __device__ __forceinline__ uint32_t drain_range_sym(const VcKernelArgs &A, uint64_t *q, uint32_t lo,
                                                     uint32_t hi, int lane, uint32_t room)
 {
+	// rounds of WAVE entries: a near-full drain takes exactly the queue's top
+	// WAVE entries (queue_append), the final drain at most VC_BIG_QCAP (the
+	// large-panel queues), so no round is spent on lanes known to be empty
+	constexpr int NR = (KEEP && !VC_DRAIN_ALL) ? 1 : (int)(VC_BIG_QCAP / WAVE);
+	constexpr bool FULL = KEEP && !VC_DRAIN_ALL;   // every lane holds an entry
+	static_assert(NR >= 1 && NR <= 4, "drain rounds");
 	uint32_t fl[4], rl[4], w[4], m[4];
 	uint64_t e64[4];
 	const uint32_t l2sh = 32u - A.l2bits;
 	const uint32_t fsh16 = 2u * (uint32_t)(A.k - 16);   // the window's first sixteen bases
 #pragma unroll
-	for (int r = 0; r < 4; ++r) {
+	for (int r = 0; r < NR; ++r) {
 		const uint32_t i = lo + (uint32_t)(r * WAVE + lane);
 		fl[r] = rl[r] = 0;
 		w[r] = 0;
 		m[r] = 1;
-		if (i < hi) {
+		if (FULL || i < hi) {
 			const uint64_t e = q[i];
 			e64[r] = e;
 			fl[r] = (uint32_t)e;
 			rl[r] = rc16(__builtin_amdgcn_alignbit((uint32_t)(e >> 32), (uint32_t)e, fsh16));
-			const uint32_t hw = vc_l2s_hash(fl[r], rl[r]);
-			m[r] = vc_l2f_mask(vc_l2s_hash2(fl[r], rl[r]));
+			// vc_l2s_hash / vc_l2s_hash2 sharing the strands' two products
+			// (the empty asm keeps the compiler from rewriting u + v as
+			// (flo + rlo) * M and multiplying again for u ^ v)
+			uint32_t u = fl[r] * VC_L2S_M, v = rl[r] * VC_L2S_M;
+			asm("" : "+v"(u), "+v"(v));
+			const uint32_t hw = vc_l2s_mix1(u, v);
+			m[r] = vc_l2f_mask(vc_l2s_mix2(u, v));
 			if constexpr ((ABL & VC_ABL_NOGATHER) != 0) asm volatile("" :: "v"(hw >> l2sh), "v"(m[r]));
 			else w[r] = A.l2f[hw >> l2sh];
 		}
@@ -414,12 +428,12 @@ __device__ __forceinline__ uint32_t drain_range_sym(const VcKernelArgs &A, uint6
 	if constexpr ((ABL & VC_ABL_NOGATHER) != 0) return 0;
 	bool surv[4];
 #pragma unroll
-	for (int r = 0; r < 4; ++r) surv[r] = (w[r] & m[r]) == m[r];   // false for empty entries (w = 0, m = 1)
+	for (int r = 0; r < NR; ++r) surv[r] = (w[r] & m[r]) == m[r];   // false for empty entries (w = 0, m = 1)
 	if constexpr (KEEP && VC_DEFER_PROBE) {
 		uint64_t bal[4];
 		uint32_t n = 0;
 #pragma unroll
-		for (int r = 0; r < 4; ++r) {
+		for (int r = 0; r < NR; ++r) {
 			bal[r] = __ballot(surv[r]);
 			n += (uint32_t)__popcll(bal[r]);
 		}
@@ -427,7 +441,7 @@ __device__ __forceinline__ uint32_t drain_range_sym(const VcKernelArgs &A, uint6
 		if (n <= room) {
 			uint32_t at = lo;
 #pragma unroll
-			for (int r = 0; r < 4; ++r) {
+			for (int r = 0; r < NR; ++r) {
 				const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[r] >> 32),
 				                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal[r], 0u));
 				if (surv[r]) q[at + pre] = e64[r];
@@ -437,7 +451,7 @@ __device__ __forceinline__ uint32_t drain_range_sym(const VcKernelArgs &A, uint6
 		}
 	}
 #pragma unroll
-	for (int r = 0; r < 4; ++r) {
+	for (int r = 0; r < NR; ++r) {
 		if (!surv[r]) continue;
 		const uint64_t key = vc_canon_from_strands(fl[r], rl[r], A.k);
 		probe_key<ABL>(A, key, vc_hash(key));
