@@ -273,6 +273,11 @@ __device__ __forceinline__ void probe_and_count(const VcKernelArgs &A, uint64_t 
 struct WaveQueue {
 	uint64_t *q;     // LDS, A.qcap entries
 	uint32_t n;      // wave-uniform fill
+	// drain_pipe (large-panel kernels): the previous near-full drain's
+	// entries, one per lane, whose second-level words are still in flight
+	uint64_t pe;     // the entry
+	uint32_t pm, pw; // its filter mask and filter word
+	bool pend;       // wave-uniform: pe / pm / pw hold a drain
 };
 
 // Probe the exact table for queue entries [lo, hi) (up to 4 per lane); the
@@ -514,6 +519,62 @@ __device__ __forceinline__ uint32_t drain_range(const VcKernelArgs &A, uint64_t 
 	return 0;
 }
 
+// Large-panel kernels: a near-full drain takes the queue's top WAVE entries
+// into registers (one per lane), hashes them and issues their second-level
+// gathers, but tests them only at the NEXT near-full drain (or the final
+// one), so the gathers' latency runs under the scan instead of stalling the
+// wave.  The previous drain's survivors go back into the queue where room
+// allows (as KEEP does), else they are probed at once.  Returns the new
+// fill.  C5 10.43-10.45 -> 10.35-10.37 ms (profiles/r05pp_ab.log);
+// -DVC_NO_PIPE_DRAIN restores drain_range<KEEP> for them.
+#ifndef VC_NO_PIPE_DRAIN
+#define VC_PIPE(ABL) (VC_SYMQ(ABL) && !VC_DRAIN_ALL && ((ABL) & (VC_ABL_NODRAIN | VC_ABL_NOGATHER)) == 0)
+#else
+#define VC_PIPE(ABL) false
+#endif
+template <int ABL>
+__device__ __forceinline__ void pipe_probe(const VcKernelArgs &A, uint64_t e)
+{
+	const uint32_t fl = (uint32_t)e;
+	const uint32_t rl = rc16(__builtin_amdgcn_alignbit((uint32_t)(e >> 32), fl, 2u * (uint32_t)(A.k - 16)));
+	const uint64_t key = vc_canon_from_strands(fl, rl, A.k);
+	probe_key<ABL>(A, key, vc_hash(key));
+}
+template <int ABL>
+__device__ __forceinline__ uint32_t drain_pipe(const VcKernelArgs &A, WaveQueue &Q, int lane)
+{
+	__builtin_amdgcn_wave_barrier();
+	const uint32_t lo = Q.n - WAVE;
+	const uint64_t e = Q.q[lo + (uint32_t)lane];
+	const uint32_t fl = (uint32_t)e;
+	const uint32_t rl = rc16(__builtin_amdgcn_alignbit((uint32_t)(e >> 32), fl, 2u * (uint32_t)(A.k - 16)));
+	uint32_t u = fl * VC_L2S_M, v = rl * VC_L2S_M;
+	asm("" : "+v"(u), "+v"(v));
+	const uint32_t m = vc_l2f_mask(vc_l2s_mix2(u, v));
+	const uint32_t w = A.l2f[vc_l2s_mix1(u, v) >> (32u - A.l2bits)];   // not awaited here
+	uint32_t n = 0;
+	if (Q.pend) {
+		const bool surv = (Q.pw & Q.pm) == Q.pm;
+		const uint64_t bal = __ballot(surv);
+		if (bal) {
+			n = (uint32_t)__popcll(bal);
+			if (n <= A.qcap - WAVE - lo) {
+				const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+				                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+				if (surv) Q.q[lo + pre] = Q.pe;
+			} else {
+				if (surv) pipe_probe<ABL>(A, Q.pe);
+				n = 0;
+			}
+		}
+	}
+	Q.pe = e;
+	Q.pm = m;
+	Q.pw = w;
+	Q.pend = true;
+	return lo + n;
+}
+
 // Lanes with `hit` append `key` (bal = ballot(hit) != 0).  The queue is
 // normally drained once per read group (queue_flush); only a nearly full
 // queue is drained here, 64 entries from its top.
@@ -526,19 +587,42 @@ __device__ __forceinline__ void queue_append(const VcKernelArgs &A, WaveQueue &Q
 	if (hit) Q.q[Q.n + pre] = key;
 	Q.n = __builtin_amdgcn_readfirstlane(Q.n + (uint32_t)__popcll(bal));
 	if (Q.n > A.qcap - WAVE) {        // A.qcap >= 2 WAVE
-		// kept survivors must leave room for one more full append (<= WAVE);
-		// VC_BIG_DRAIN_ALL (A/B): the large-panel kernels drain the whole queue
-		const uint32_t lo = (VC_SYMQ(ABL) && VC_DRAIN_ALL) ? 0u : Q.n - WAVE;
-		Q.n = lo + drain_range<ABL, true>(A, Q.q, lo, Q.n, lane, A.qcap - WAVE - lo);
-		// leave nothing in flight on this (rare) path, so that the compiler
-		// can keep counting the scan's prefetches across it
-		__builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+		if constexpr (VC_PIPE(ABL)) {
+			Q.n = drain_pipe<ABL>(A, Q, lane);
+		} else {
+			// kept survivors must leave room for one more full append (<= WAVE);
+			// VC_BIG_DRAIN_ALL (A/B): the large-panel kernels drain the whole queue
+			const uint32_t lo = (VC_SYMQ(ABL) && VC_DRAIN_ALL) ? 0u : Q.n - WAVE;
+			Q.n = lo + drain_range<ABL, true>(A, Q.q, lo, Q.n, lane, A.qcap - WAVE - lo);
+			// leave nothing in flight on this (rare) path, so that the compiler
+			// can keep counting the scan's prefetches across it
+			__builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+		}
 	}
 }
 
 template <int ABL>
 __device__ __forceinline__ void queue_flush(const VcKernelArgs &A, WaveQueue &Q, int lane)
 {
+	if constexpr (VC_PIPE(ABL)) {
+		// the pending drain's survivors join the final drain where they fit
+		if (Q.pend) {
+			const bool surv = (Q.pw & Q.pm) == Q.pm;
+			const uint64_t bal = __ballot(surv);
+			if (bal) {
+				const uint32_t n = (uint32_t)__popcll(bal);
+				if (Q.n + n <= A.qcap) {
+					const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+					                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+					if (surv) Q.q[Q.n + pre] = Q.pe;
+					Q.n += n;
+				} else if (surv) {
+					pipe_probe<ABL>(A, Q.pe);
+				}
+			}
+			Q.pend = false;
+		}
+	}
 	if (Q.n) drain_range<ABL>(A, Q.q, 0, Q.n, lane);
 	Q.n = 0;
 }
@@ -1890,6 +1974,7 @@ vc_count_reads_kernel(VcKernelArgs A)
 	WaveQueue Q;
 	Q.q = reinterpret_cast<uint64_t *>(smem + vc_filter_lds_words(A.fwords)) + wave * A.qcap;
 	Q.n = 0;
+	Q.pend = false;
 	load_filter(A, filt);
 
 	const uint32_t *s32 = reinterpret_cast<const uint32_t *>(A.seq);
@@ -1966,6 +2051,7 @@ vc_count_long_kernel(VcKernelArgs A)
 	WaveQueue Q;
 	Q.q = reinterpret_cast<uint64_t *>(smem + vc_filter_lds_words(A.fwords)) + wave * A.qcap;
 	Q.n = 0;
+	Q.pend = false;
 	load_filter(A, filt);
 
 	const uint32_t *s32 = reinterpret_cast<const uint32_t *>(A.seq);
