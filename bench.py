@@ -100,8 +100,8 @@ LIMITER_LARGE_PANEL = ("the roofline is HBM (integer byte work, no MFMA); the la
                        "an ablation puts 57 % of the time in the scan (Bloom lookups at 9 VALU a window), 15 % in "
                        "the hit loop, 10 % in the drains' arithmetic, 15 % in the gathers into the L2-resident "
                        "second-level filter (64 distinct lines per instruction) and 3 % in the exact-table probes; "
-                       "21.7 VALU per base (5.10 G per launch), TA busy 3.72 G cycles over 256 CUs; DESIGN.md "
-                       "section 3.1.3, profiles/r05v2_c5_pmc_counters.json, profiles/r05l_abl_time.log")
+                       "21.4 VALU per base (5.01 G per launch), TA busy 3.73 G cycles over 256 CUs; DESIGN.md "
+                       "section 3.1.3, profiles/r05v3_c5_pmc_counters.json, profiles/r05ab_abl_time.log")
 
 
 def cli_run(binary, pat, fq, threads, out, k, env=None, timeout=900):
