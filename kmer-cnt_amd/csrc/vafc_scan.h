@@ -275,9 +275,9 @@ struct WaveQueue {
 	uint32_t n;      // wave-uniform fill
 	// drain_pipe (large-panel kernels): the previous near-full drain's
 	// entries, one per lane, whose second-level words are still in flight
-	uint64_t pe;     // the entry
-	uint32_t pm, pw; // its filter mask and filter word
-	bool pend;       // wave-uniform: pe / pm / pw hold a drain
+	uint64_t pe[2];     // the entries (VC_PIPE_ROUNDS of them per lane)
+	uint32_t pm[2], pw[2];  // their filter masks and filter words (empty: pm = 1, pw = 0)
+	bool pend;          // wave-uniform: pe / pm / pw hold a drain
 };
 
 // Probe the exact table for queue entries [lo, hi) (up to 4 per lane); the
@@ -540,37 +540,71 @@ __device__ __forceinline__ void pipe_probe(const VcKernelArgs &A, uint64_t e)
 	const uint64_t key = vc_canon_from_strands(fl, rl, A.k);
 	probe_key<ABL>(A, key, vc_hash(key));
 }
+// VC_PIPE_ROUNDS = 2 (A/B): the drain takes the whole queue (65..128
+// entries, two per lane) instead of its top 64: 10.72 against 10.35 ms
+// (profiles/r05p2_ab.log), not the default.
+#ifndef VC_PIPE_ROUNDS
+#define VC_PIPE_ROUNDS 1
+#endif
 template <int ABL>
 __device__ __forceinline__ uint32_t drain_pipe(const VcKernelArgs &A, WaveQueue &Q, int lane)
 {
+	constexpr int PR = VC_PIPE_ROUNDS;
+	static_assert(PR == 1 || PR == 2, "pipe rounds");
 	__builtin_amdgcn_wave_barrier();
-	const uint32_t lo = Q.n - WAVE;
-	const uint64_t e = Q.q[lo + (uint32_t)lane];
-	const uint32_t fl = (uint32_t)e;
-	const uint32_t rl = rc16(__builtin_amdgcn_alignbit((uint32_t)(e >> 32), fl, 2u * (uint32_t)(A.k - 16)));
-	uint32_t u = fl * VC_L2S_M, v = rl * VC_L2S_M;
-	asm("" : "+v"(u), "+v"(v));
-	const uint32_t m = vc_l2f_mask(vc_l2s_mix2(u, v));
-	const uint32_t w = A.l2f[vc_l2s_mix1(u, v) >> (32u - A.l2bits)];   // not awaited here
+	const uint32_t lo = PR == 1 ? Q.n - WAVE : 0u;   // PR = 2: Q.n > WAVE, so round 0 is full
+	uint64_t e[PR];
+	uint32_t m[PR], w[PR];
+#pragma unroll
+	for (int r = 0; r < PR; ++r) {
+		const uint32_t i = lo + (uint32_t)(r * WAVE + lane);
+		e[r] = 0;
+		m[r] = 1;
+		w[r] = 0;
+		if (r == 0 || i < Q.n) {
+			e[r] = Q.q[i];
+			const uint32_t fl = (uint32_t)e[r];
+			const uint32_t rl = rc16(__builtin_amdgcn_alignbit((uint32_t)(e[r] >> 32), fl, 2u * (uint32_t)(A.k - 16)));
+			uint32_t u = fl * VC_L2S_M, v = rl * VC_L2S_M;
+			asm("" : "+v"(u), "+v"(v));
+			m[r] = vc_l2f_mask(vc_l2s_mix2(u, v));
+			w[r] = A.l2f[vc_l2s_mix1(u, v) >> (32u - A.l2bits)];   // not awaited here
+		}
+	}
 	uint32_t n = 0;
 	if (Q.pend) {
-		const bool surv = (Q.pw & Q.pm) == Q.pm;
-		const uint64_t bal = __ballot(surv);
-		if (bal) {
-			n = (uint32_t)__popcll(bal);
+		bool surv[PR];
+		uint64_t bal[PR];
+#pragma unroll
+		for (int r = 0; r < PR; ++r) {
+			surv[r] = (Q.pw[r] & Q.pm[r]) == Q.pm[r];   // false for empty slots (pw = 0, pm = 1)
+			bal[r] = __ballot(surv[r]);
+			n += (uint32_t)__popcll(bal[r]);
+		}
+		if (n) {
 			if (n <= A.qcap - WAVE - lo) {
-				const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-				                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-				if (surv) Q.q[lo + pre] = Q.pe;
+				uint32_t at = lo;
+#pragma unroll
+				for (int r = 0; r < PR; ++r) {
+					const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[r] >> 32),
+					                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal[r], 0u));
+					if (surv[r]) Q.q[at + pre] = Q.pe[r];
+					at += (uint32_t)__popcll(bal[r]);
+				}
 			} else {
-				if (surv) pipe_probe<ABL>(A, Q.pe);
+#pragma unroll
+				for (int r = 0; r < PR; ++r)
+					if (surv[r]) pipe_probe<ABL>(A, Q.pe[r]);
 				n = 0;
 			}
 		}
 	}
-	Q.pe = e;
-	Q.pm = m;
-	Q.pw = w;
+#pragma unroll
+	for (int r = 0; r < PR; ++r) {
+		Q.pe[r] = e[r];
+		Q.pm[r] = m[r];
+		Q.pw[r] = w[r];
+	}
 	Q.pend = true;
 	return lo + n;
 }
@@ -607,17 +641,20 @@ __device__ __forceinline__ void queue_flush(const VcKernelArgs &A, WaveQueue &Q,
 	if constexpr (VC_PIPE(ABL)) {
 		// the pending drain's survivors join the final drain where they fit
 		if (Q.pend) {
-			const bool surv = (Q.pw & Q.pm) == Q.pm;
-			const uint64_t bal = __ballot(surv);
-			if (bal) {
-				const uint32_t n = (uint32_t)__popcll(bal);
-				if (Q.n + n <= A.qcap) {
-					const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-					                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-					if (surv) Q.q[Q.n + pre] = Q.pe;
-					Q.n += n;
-				} else if (surv) {
-					pipe_probe<ABL>(A, Q.pe);
+#pragma unroll
+			for (int r = 0; r < VC_PIPE_ROUNDS; ++r) {
+				const bool surv = (Q.pw[r] & Q.pm[r]) == Q.pm[r];
+				const uint64_t bal = __ballot(surv);
+				if (bal) {
+					const uint32_t n = (uint32_t)__popcll(bal);
+					if (Q.n + n <= A.qcap) {
+						const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+						                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+						if (surv) Q.q[Q.n + pre] = Q.pe[r];
+						Q.n += n;
+					} else if (surv) {
+						pipe_probe<ABL>(A, Q.pe[r]);
+					}
 				}
 			}
 			Q.pend = false;
