@@ -1296,7 +1296,7 @@ __device__ __forceinline__ void packed_streams(const VcKernelArgs &A, int c, int
 		// the first window (ending at K - 1) starts with the 10-mer ending at
 		// base 9: chunk 0's bases 9..15 are looked up for the later windows
 		static_assert(K - VC_FLANK_BASES >= 9, "flank mode needs the first window's head in chunk 0");
-		if constexpr (VC_FLANK_U8) H = flank_bits_u8<VC_FLANK_BASES - 1, 16, ABL>(Bm1, Bc);
+		if constexpr (VC_FLANK_U8) H = flank_bits_u8_grouped<VC_FLANK_BASES - 1, 16, ABL>(Bm1, Bc);
 		else H = flank_bits<VC_FLANK_BASES - 1, 16, ABL>(lds_base(filt), Bm1, Bc);
 	}
 	Bm2 = Bm1; Bm1 = Bc;
@@ -1780,7 +1780,7 @@ __device__ __forceinline__ void packed_streams_fb(const VcKernelArgs &A, const D
 	}
 	const uint32_t Bc = pack_fb(D, t0, t1, t2, t3);
 	static_assert(K - VC_FLANK_BASES >= 9, "flank mode needs the first window's head in chunk 0");
-	if constexpr (VC_FLANK_U8) H = flank_bits_u8<VC_FLANK_BASES - 1, 16, ABL>(Bm1, Bc);
+	if constexpr (VC_FLANK_U8) H = flank_bits_u8_grouped<VC_FLANK_BASES - 1, 16, ABL>(Bm1, Bc);
 	else H = flank_bits<VC_FLANK_BASES - 1, 16, ABL>(0u, Bm1, Bc);
 	Bm2 = Bm1; Bm1 = Bc;
 }
