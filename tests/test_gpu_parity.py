@@ -246,6 +246,25 @@ def test_second_level_filter_threshold(k, n_sel):
     assert int(want.sum()) > 50_000
 
 
+@pytest.mark.parametrize("k", list(range(21, 32)))
+def test_large_panel_kernels_every_k(k):
+    """The large-panel kernels (144 KiB LDS filter, strand-keyed second-level
+    filter, pipelined near-full drains) for every k they are built for, on a
+    read set dense in keys (about a quarter of the windows are keys): the
+    drains' survivors often overflow the room kept for them, so the
+    probe-at-once paths run too.  Counts equal the oracle's."""
+    rng = np.random.default_rng(3000 + k)
+    reads = [np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, int(L))].tobytes()
+             for L in rng.integers(100, 300, 1500)]
+    reads += random_reads(rng, list(rng.integers(0, 400, 300)))   # odd bytes, short and long reads
+    keys, vals, n_pat = table_from_reads(k, reads, rng, n_pat=70_000)
+    got, km = gpu_counts(k, keys, vals, n_pat, reads, blocks=2)
+    want, km_want = oracle_counts(k, keys, vals, n_pat, reads)
+    assert km == km_want
+    assert np.array_equal(got, want)
+    assert int(want.sum()) > 50_000
+
+
 @pytest.mark.parametrize("k", [1, 5, 15, 16, 17, 21, 31])
 def test_every_kmer_of_golden_reads(k):
     """Table = every distinct k-mer of the golden reads (whose k-mer lists are pinned
