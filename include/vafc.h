@@ -245,6 +245,18 @@ int vc_scan_file_range(const char *path, int k, int block_bases, int n_threads, 
  * the pieces of that pass (0: none yet).  prof may be NULL. */
 uint64_t vc_ingest_profile(double *prof);
 
+/* The same pass's profile with the workers' parse split (round 6): the first
+ * min(n, VC_INGEST_PROFILE_FIELDS) of prof[] = the seven fields above, then
+ * the workers' seconds reading the source (pread: the copy out of the page
+ * cache) and the bytes read, seconds copying accepted sequences into the slots
+ * and the bytes copied (0 with VAFC_SLOT_COPY=0, which copies per read
+ * untimed), seconds guessing record starts, the workers' CPU seconds and
+ * wall seconds (CPU < wall: descheduled, e.g. a CPU quota's throttling), the
+ * main thread's CPU seconds, the worker count and the slot-copy mode.
+ * Returns the pieces of that pass. */
+#define VC_INGEST_PROFILE_FIELDS 17
+uint64_t vc_ingest_profile_ex(double *prof, int n);
+
 /* Optional: allocate vc_count_file's parallel-reader buffers for n_threads
  * reader threads now (pinned host + device memory, about 20 MB per thread),
  * so that a later vc_count_file does not pay for the allocation.  Without

@@ -180,6 +180,7 @@ bool VcFastqReader::refill()
 	}
 	ssize_t n;
 	if (src_) {
+		if (refill_fn_) refill_fn_(refill_arg_);
 		n = (ssize_t)src_->read(buf_, cap_, foff_);
 		base_ = foff_;
 		if (n > 0) foff_ += (uint64_t)n;

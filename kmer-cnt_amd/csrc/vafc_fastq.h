@@ -91,6 +91,16 @@ public:
 	size_t seq_len() const { return seqp_ ? seql_ : seq_.l; }
 	// keep record names (kseq's name: the header up to the first isspace byte)
 	void keep_names(bool on) { keep_name_ = on; }
+	// Called before an owned window (open_src) is overwritten by the next
+	// source read: sequences handed out as pointers into it are still valid
+	// inside the call (the parallel reader's batched slot copy, vafc_ingest.cpp).
+	void on_refill(void (*fn)(void *), void *arg)
+	{
+		refill_fn_ = fn;
+		refill_arg_ = arg;
+	}
+	// seq() points into the window (valid until the window is refilled)
+	bool seq_in_window() const { return seqp_ != nullptr; }
 	const char *name() const { return name_.s ? name_.s : ""; }
 	size_t name_len() const { return name_.l; }
 
@@ -110,6 +120,8 @@ private:
 	uint64_t hdr_pos_ = 0;        // its text offset (source reads)
 	VcByteBuf seq_, name_;
 	bool keep_name_ = false;
+	void (*refill_fn_)(void *) = nullptr;
+	void *refill_arg_ = nullptr;
 
 	bool refill();
 	inline int getc_()

@@ -1450,11 +1450,15 @@ extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n
 	vc_file_stats local = {0, 0, 0, 0.0};
 	const double t0 = wall_now();
 	HIPCK(hipSetDevice(c->dev));
-	const int fd = open(path, O_RDONLY);
-	if (fd < 0) return VC_EIO;
+	// a path that is not a regular file (a FIFO, a device) is opened exactly
+	// once, by the sequential reader below: opening it here only to look at
+	// it would let a pipe's writer see its reader go away
 	struct stat sb;
+	if (stat(path, &sb) != 0) return VC_EIO;
+	const int fd = S_ISREG(sb.st_mode) ? open(path, O_RDONLY) : -1;
+	if (S_ISREG(sb.st_mode) && fd < 0) return VC_EIO;
 	uint8_t magic[2] = {0, 0};
-	const bool reg = fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
+	const bool reg = fd >= 0 && fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
 	const bool gz = reg && pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
 	const bool plain = reg && !gz;
 	// the reader threads spawned below run on the GPU's NUMA node when it has
@@ -1473,7 +1477,7 @@ extern "C" int vc_count_file(vc_ctx *c, const char *path, int block_bases, int n
 			if (st) *st = local;
 			return rc;
 		}
-		close(fd);
+		if (fd >= 0) close(fd);
 		if (gz) {   // parallel inflate + parallel parse (falls through if the inflater declines the file)
 			const char *ce = getenv("VAFC_GZ_CHUNK");            // test knob: compressed bytes per chunk
 			VcGzParallel *g = vc_gzp_open(path, vc_gz_inflate_threads(clamp_threads(n_threads)),
@@ -1507,14 +1511,17 @@ extern "C" int vc_count_file_range(vc_ctx *c, const char *path, uint64_t begin, 
 	vc_file_stats local = {0, 0, 0, 0.0};
 	*ri = vc_range_info{UINT64_MAX, UINT64_MAX, 0, 0, 1};
 	const double t0 = wall_now();
-	const int fd = open(path, O_RDONLY);
-	if (fd < 0) return VC_EIO;
 	struct stat sb;
+	if (stat(path, &sb) != 0) return VC_EIO;
+	// not a regular file (a FIFO): never opened here, so vc_count_file's
+	// reader is its only reader (a pipe is read once, as the reference does)
+	const int fd = S_ISREG(sb.st_mode) ? open(path, O_RDONLY) : -1;
+	if (S_ISREG(sb.st_mode) && fd < 0) return VC_EIO;
 	uint8_t magic[2] = {0, 0};
-	const bool reg = fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
+	const bool reg = fd >= 0 && fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
 	const bool gz = reg && pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
 	if (!reg || gz) {   // not split: the first range counts the whole file
-		close(fd);
+		if (fd >= 0) close(fd);
 		if (begin > 0) {
 			if (st) *st = local;
 			return VC_OK;

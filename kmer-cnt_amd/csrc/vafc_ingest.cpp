@@ -8,6 +8,7 @@
 #include <string.h>
 #include <time.h>
 #include <sys/mman.h>
+#include <immintrin.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -35,6 +36,21 @@ struct Piece {
 	bool ready = false;
 };
 
+double ing_clock(clockid_t id)
+{
+	struct timespec ts;
+	clock_gettime(id, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+// Per-thread tallies of the reads out of a plain file (the copy out of the
+// page cache): seconds and bytes, reset by each worker when it starts.
+struct IoTally {
+	double read_s = 0;
+	uint64_t read_bytes = 0;
+};
+thread_local IoTally io_tally;
+
 ssize_t pread_full(int fd, uint8_t *p, size_t n, uint64_t off)
 {
 	size_t got = 0;
@@ -46,6 +62,122 @@ ssize_t pread_full(int fd, uint8_t *p, size_t n, uint64_t off)
 	}
 	return (ssize_t)got;
 }
+
+// How accepted sequences reach the slot (VAFC_SLOT_COPY): 0 one memcpy per
+// read as it is parsed; 1 the same copies deferred and done in batches of
+// about 32 KiB (or before the reader's window is refilled), so their time is
+// measured; 2 batches gathered in a small L1-resident stage and written to the
+// slot with non-temporal stores, whole 64-byte lines only (the slot is read
+// next by the DMA engine, not the CPU: regular stores first read every
+// destination line from DRAM for ownership).
+int slot_copy_mode()   // read once per pass (A/B passes in one process)
+{
+	const char *e = getenv("VAFC_SLOT_COPY");
+	return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
+}
+
+class SlotCopier {
+public:
+	explicit SlotCopier(int mode) : mode_(mode) {}
+	void bind(uint8_t *dst) { dst_ = dst; }
+	// sequence [src, src + len) goes to dst + at; in_window: src stays valid
+	// until the reader's window is refilled (else: only until the next record)
+	void add(const char *src, size_t len, uint64_t at, bool in_window)
+	{
+		if (mode_ == 0) {
+			memcpy(dst_ + at, src, len);
+			return;
+		}
+		if (!in_window || len > kStage / 2) {   // the reader's own copy, or a very long read
+			flush();
+			const double t0 = ing_clock(CLOCK_MONOTONIC);
+			memcpy(dst_ + at, src, len);
+			secs += ing_clock(CLOCK_MONOTONIC) - t0;
+			bytes += len;
+			return;
+		}
+		if (!ents_.empty() && (pend_ + len > kStage || at != d1_)) flush();
+		if (ents_.empty()) d0_ = d1_ = at;
+		ents_.push_back({(const uint8_t *)src, (uint32_t)len});
+		d1_ += len;
+		pend_ += len;
+		if (pend_ >= kStage / 2) flush();
+	}
+	void flush()
+	{
+		if (ents_.empty()) return;
+		const double t0 = ing_clock(CLOCK_MONOTONIC);
+		uint8_t *d = dst_ + d0_;
+		if (mode_ == 1) {
+			for (const Ent &e : ents_) {
+				memcpy(d, e.src, e.len);
+				d += e.len;
+			}
+		} else {
+			uint8_t *s = stage_;
+			for (const Ent &e : ents_) {
+				memcpy(s, e.src, e.len);
+				s += e.len;
+			}
+			stream(d, stage_, pend_);
+		}
+		secs += ing_clock(CLOCK_MONOTONIC) - t0;
+		bytes += pend_;
+		ents_.clear();
+		pend_ = 0;
+	}
+	// end of a piece: everything written and the streaming stores ordered
+	// before the piece is handed to the main thread
+	void finish()
+	{
+		flush();
+		if (mode_ == 2) _mm_sfence();
+	}
+	static void refill_hook(void *self) { ((SlotCopier *)self)->flush(); }
+	double secs = 0;
+	uint64_t bytes = 0;
+
+private:
+	struct Ent {
+		const uint8_t *src;
+		uint32_t len;
+	};
+	static constexpr size_t kStage = (size_t)32 << 10;
+	int mode_;
+	uint8_t *dst_ = nullptr;
+	std::vector<Ent> ents_;
+	uint64_t d0_ = 0, d1_ = 0;
+	size_t pend_ = 0;
+	alignas(64) uint8_t stage_[kStage];
+
+	// n bytes from s to d: the partial lines at either end with regular
+	// stores, every whole 64-byte line of d in between with streaming stores
+	__attribute__((target("avx2"))) static void stream_avx2(uint8_t *d, const uint8_t *s, size_t n)
+	{
+		const size_t head = (size_t)((64 - ((uintptr_t)d & 63)) & 63);
+		if (n < head + 64) {
+			memcpy(d, s, n);
+			return;
+		}
+		memcpy(d, s, head);
+		d += head;
+		s += head;
+		n -= head;
+		for (; n >= 64; n -= 64, d += 64, s += 64) {
+			const __m256i a = _mm256_loadu_si256((const __m256i *)s);
+			const __m256i b = _mm256_loadu_si256((const __m256i *)(s + 32));
+			_mm256_stream_si256((__m256i *)d, a);
+			_mm256_stream_si256((__m256i *)(d + 32), b);
+		}
+		memcpy(d, s, n);
+	}
+	static void stream(uint8_t *d, const uint8_t *s, size_t n)
+	{
+		static const bool avx2 = __builtin_cpu_supports("avx2");
+		if (avx2) stream_avx2(d, s, n);
+		else memcpy(d, s, n);
+	}
+};
 
 // A plain file through pread into each worker's window.  VAFC_MMAP=1 maps
 // the file instead and the workers parse the page cache in place
@@ -72,11 +204,19 @@ public:
 	}
 	int64_t read(uint8_t *p, size_t n, uint64_t off) override
 	{
-		if (!map_) return pread_full(fd_, p, n, off);
-		if (off >= size_) return 0;
-		const size_t got = size_ - off < n ? (size_t)(size_ - off) : n;
-		memcpy(p, map_ + off, got);
-		return (int64_t)got;
+		const double t0 = ing_clock(CLOCK_MONOTONIC);
+		int64_t got;
+		if (!map_) {
+			got = pread_full(fd_, p, n, off);
+		} else if (off >= size_) {
+			got = 0;
+		} else {
+			got = (int64_t)(size_ - off < n ? (size_t)(size_ - off) : n);
+			memcpy(p, map_ + off, (size_t)got);
+		}
+		io_tally.read_s += ing_clock(CLOCK_MONOTONIC) - t0;
+		io_tally.read_bytes += got > 0 ? (uint64_t)got : 0;
+		return got;
 	}
 	const uint8_t *view(uint64_t off, uint64_t *avail) override
 	{
@@ -245,28 +385,16 @@ const uint8_t *find_nl(const uint8_t *p, const uint8_t *e)
 	return p < e ? (const uint8_t *)memchr(p, '\n', (size_t)(e - p)) : nullptr;
 }
 
-// First plausible record header at or after a (a > 0), or -1.  FASTQ: a line
-// "@..." followed by a sequence line, a '+' line and a quality line of the
-// same length, then '@' or end of input.  FASTA: any line starting with '>'
-// or '@' (kseq ends a FASTA record at either).  Only a guess: the caller
-// checks it against the previous piece's end.
-int64_t guess_record(VcTextSource &src, uint64_t a, bool fasta, std::vector<uint8_t> &tmp)
+// First plausible record header in s[1, n) (s = the text from offset
+// `from`), or -1 when none is decided inside those n bytes (at_eof: they end
+// the text).  FASTQ: a line "@..." followed by a sequence line, a '+' line and
+// a quality line of the same length, then '@' or end of input.  FASTA: any line
+// starting with '>' or '@' (kseq ends a FASTA record at either).  A candidate is
+// accepted or rejected only on bytes inside the buffer, so a longer buffer can
+// only turn a -1 into an answer, never change an answer.
+int64_t guess_in(const uint8_t *s, size_t n, uint64_t from, bool at_eof, bool fasta)
 {
-	const uint64_t from = a - 1;
-	const size_t want = (size_t)1 << 20;
-	uint64_t avail = 0;
-	const uint8_t *s = src.view(from, &avail);
-	int64_t got;
-	if (s) {
-		got = (int64_t)(avail < want ? avail : want);
-	} else {
-		tmp.resize(want);
-		got = src.read(tmp.data(), want, from);
-		s = tmp.data();
-	}
-	if (got < 2) return -1;
-	const uint8_t *e = s + got;
-	const bool at_eof = (size_t)got < want;   // a short read ends at the end of the text
+	const uint8_t *e = s + n;
 	for (const uint8_t *p = s + 1; p < e; ++p) {
 		if (p[-1] != '\n') {
 			p = find_nl(p, e);
@@ -281,7 +409,11 @@ int64_t guess_record(VcTextSource &src, uint64_t a, bool fasta, std::vector<uint
 		const uint8_t *n1 = find_nl(p, e);
 		const uint8_t *n2 = n1 ? find_nl(n1 + 1, e) : nullptr;
 		if (!n2) return -1;
-		if (n2 + 1 >= e || n2[1] != '+') continue;
+		if (n2 + 1 >= e) {
+			if (!at_eof) return -1;
+			continue;
+		}
+		if (n2[1] != '+') continue;
 		const uint8_t *n3 = find_nl(n2 + 1, e);
 		if (!n3) return -1;
 		const uint8_t *n4 = find_nl(n3 + 1, e);
@@ -295,10 +427,38 @@ int64_t guess_record(VcTextSource &src, uint64_t a, bool fasta, std::vector<uint
 	return -1;
 }
 
+// First plausible record header at or after a (a > 0), or -1, looked for in
+// the 1 MiB of text from a - 1.  Only a guess: the caller checks it against
+// the previous piece's end.  The text is read in growing steps (16 KiB, 128
+// KiB, 1 MiB) until guess_in decides: a FASTQ record is a few hundred bytes,
+// and reading the whole MiB per piece was 6 % of the bytes the workers copied
+// out of the page cache (round 6, profiles/r06a_split.json).
+int64_t guess_record(VcTextSource &src, uint64_t a, bool fasta, std::vector<uint8_t> &tmp)
+{
+	const uint64_t from = a - 1;
+	const size_t cap = (size_t)1 << 20;
+	uint64_t avail = 0;
+	const uint8_t *v = src.view(from, &avail);
+	if (v) {
+		const size_t got = (size_t)(avail < cap ? avail : cap);
+		return got < 2 ? -1 : guess_in(v, got, from, got < cap, fasta);
+	}
+	tmp.resize(cap);
+	size_t have = 0;
+	for (size_t want = (size_t)16 << 10;; want = want * 8 < cap ? want * 8 : cap) {
+		const int64_t got = src.read(tmp.data() + have, want - have, from + have);
+		have += got > 0 ? (size_t)got : 0;
+		const bool at_eof = have < want;   // a short read ends at the end of the text
+		if (have < 2) return -1;
+		const int64_t g = guess_in(tmp.data(), have, from, at_eof, fasta);
+		if (g >= 0 || at_eof || want == cap) return g;
+	}
+}
+
 // Parse records whose header lies in [start, P.b) (kseq semantics from a
 // record boundary) into the piece's slot.
 int parse_piece(VcTextSource &src, uint64_t start, int k, int slot, VcIngestSink &sink, VcFastqReader &rd,
-                Piece &P)
+                Piece &P, SlotCopier &cp)
 {
 	P.start = (int64_t)start;
 	P.n = P.bytes = 0;
@@ -310,6 +470,17 @@ int parse_piece(VcTextSource &src, uint64_t start, int k, int slot, VcIngestSink
 	const char *we = getenv("VAFC_READER_WINDOW");   // test knob: the workers' window in bytes
 	const size_t win = we && atoll(we) > 0 ? (size_t)atoll(we) : (size_t)1 << 20;
 	if (!(v ? rd.open_view(v, avail, start) : rd.open_src(&src, start, win))) return VC_ENOMEM;
+	cp.bind(P.buf.seq);
+	rd.on_refill(SlotCopier::refill_hook, &cp);
+	struct Unhook {   // every pending copy done and the hook gone, however the piece ends
+		VcFastqReader &r;
+		SlotCopier &c;
+		~Unhook()
+		{
+			c.finish();
+			r.on_refill(nullptr, nullptr);
+		}
+	} unhook{rd, cp};
 	size_t used = 0;
 	for (;;) {
 		const int64_t h = rd.peek_header();
@@ -338,10 +509,12 @@ int parse_piece(VcTextSource &src, uint64_t start, int k, int slot, VcIngestSink
 			size_t nb = P.buf.cap_bytes, nr = P.buf.cap_reads;
 			while (used + len > nb) nb = nb * 2 + len;
 			while (P.n + 1 > nr) nr = nr * 2 + 1024;
+			cp.flush();   // the pending sequences into the old buffers, which grow() copies
 			int rc = sink.grow(slot, &P.buf, nb, nr, used, (size_t)P.n);
 			if (rc != VC_OK) return rc;
+			cp.bind(P.buf.seq);
 		}
-		memcpy(P.buf.seq + used, rd.seq(), len);
+		cp.add(rd.seq(), len, used, rd.seq_in_window());
 		P.buf.offs[P.n] = used;
 		P.buf.lens[P.n] = (uint32_t)len;
 		used += len;
@@ -412,6 +585,7 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 	// timings are always taken (a few clock reads per piece of megabytes);
 	// VAFC_INGEST_PROFILE also prints them
 	const bool prof_print = getenv("VAFC_INGEST_PROFILE") != nullptr;
+	const int copy_mode = slot_copy_mode();
 	vc_ingest_last = VcIngestProfile();
 	double t_wait = 0, t_submit = 0, t_reparse = 0;
 	std::atomic<uint64_t> t_parse_us{0}, t_slotwait_us{0}, t_acquire_us{0};
@@ -454,10 +628,10 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 	std::atomic<uint64_t> next{0};
 
 	const VcCpuSet cpus = vc_affinity_get();   // vc_count_file's placement (vafc_affinity.h)
-	auto worker = [&]() {
-		vc_affinity_bind(cpus);
-		VcFastqReader rd;
-		std::vector<uint8_t> tmp;
+	// the workers' own tallies, added up as each worker ends
+	std::atomic<uint64_t> w_read_ns{0}, w_read_bytes{0}, w_copy_ns{0}, w_copy_bytes{0}, w_guess_ns{0};
+	std::atomic<uint64_t> w_cpu_ns{0}, w_wall_ns{0};
+	auto worker_loop = [&](VcFastqReader &rd, std::vector<uint8_t> &tmp, SlotCopier &cp) {
 		for (;;) {
 			const uint64_t j = next.fetch_add(1);
 			const double w0 = ing_now();
@@ -483,8 +657,10 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 			int rc = sink.acquire(slot, &P.buf);
 			t_acquire_us += (uint64_t)((ing_now() - w1) * 1e6);
 			if (rc == VC_OK) {
+				const double g0 = ing_now();
 				const int64_t g = P.a == 0 ? 0 : guess_record(src, P.a, fasta, tmp);
-				if (g >= 0) rc = parse_piece(src, (uint64_t)g, k, slot, sink, rd, P);
+				w_guess_ns += (uint64_t)((ing_now() - g0) * 1e9);
+				if (g >= 0) rc = parse_piece(src, (uint64_t)g, k, slot, sink, rd, P, cp);
 				else P.start = -1;
 			}
 			{
@@ -498,6 +674,22 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 			cv.notify_all();
 		}
 	};
+	auto worker = [&]() {
+		vc_affinity_bind(cpus);
+		const double c0 = ing_clock(CLOCK_THREAD_CPUTIME_ID), t0 = ing_now();
+		io_tally = IoTally();
+		VcFastqReader rd;
+		std::vector<uint8_t> tmp;
+		SlotCopier cp(copy_mode);
+		worker_loop(rd, tmp, cp);
+		w_read_ns += (uint64_t)(io_tally.read_s * 1e9);
+		w_read_bytes += io_tally.read_bytes;
+		w_copy_ns += (uint64_t)(cp.secs * 1e9);
+		w_copy_bytes += cp.bytes;
+		w_cpu_ns += (uint64_t)((ing_clock(CLOCK_THREAD_CPUTIME_ID) - c0) * 1e9);
+		w_wall_ns += (uint64_t)((ing_now() - t0) * 1e9);
+	};
+	const double main_cpu0 = ing_clock(CLOCK_THREAD_CPUTIME_ID);
 	std::vector<std::thread> pool;
 	for (int t = 0; t < threads; ++t) pool.emplace_back(worker);
 
@@ -506,6 +698,7 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 	uint64_t expect = 0;              // where the next record's header is
 	uint64_t np = 0;
 	VcFastqReader rd;
+	SlotCopier mcp(copy_mode);   // the main thread's re-parses
 	for (uint64_t j = 0;; ++j) {
 		const int slot = (int)(j % (uint64_t)slots);
 		Piece &P = pcs[(size_t)slot];
@@ -537,7 +730,7 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 		if (rc == VC_OK && !S.stopped && P.b > expect) {
 			if (P.start < 0 || (uint64_t)P.start != expect) { // a wrong guess: parse from the true boundary
 				const double r0 = ing_now();
-				rc = parse_piece(src, expect, k, slot, sink, rd, P);
+				rc = parse_piece(src, expect, k, slot, sink, rd, P, mcp);
 				t_reparse += ing_now() - r0;
 			}
 			if (rc == VC_OK) {
@@ -579,12 +772,25 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 		L.acquire = t_acquire_us.load() * 1e-6;
 		L.pieces = np;
 		L.threads = threads;
+		L.read_s = w_read_ns.load() * 1e-9;
+		L.read_bytes = w_read_bytes.load();
+		L.copy_s = w_copy_ns.load() * 1e-9;
+		L.copy_bytes = w_copy_bytes.load();
+		L.guess_s = w_guess_ns.load() * 1e-9;
+		L.worker_cpu = w_cpu_ns.load() * 1e-9;
+		L.worker_wall = w_wall_ns.load() * 1e-9;
+		L.main_cpu = ing_clock(CLOCK_THREAD_CPUTIME_ID) - main_cpu0;
+		L.copy_mode = copy_mode;
 	}
-	if (prof_print)
-		fprintf(stderr, "[ingest] %llu pieces, %d threads: total %.3f s; main: wait %.3f submit %.3f reparse %.3f; "
-		        "workers: parse %.3f slot-wait %.3f acquire %.3f (thread-seconds)\n", (unsigned long long)np, threads,
-		        vc_ingest_last.total, t_wait, t_submit, t_reparse, vc_ingest_last.parse, vc_ingest_last.slot_wait,
-		        vc_ingest_last.acquire);
+	if (prof_print) {
+		const VcIngestProfile &L = vc_ingest_last;
+		fprintf(stderr, "[ingest] %llu pieces, %d threads: total %.3f s; main: wait %.3f submit %.3f reparse %.3f "
+		        "cpu %.3f; workers: parse %.3f slot-wait %.3f acquire %.3f (thread-seconds); parse split: read %.3f "
+		        "(%.2f GB) copy %.3f (%.2f GB, mode %d) guess %.3f; workers cpu %.3f of wall %.3f\n",
+		        (unsigned long long)np, threads, L.total, t_wait, t_submit, t_reparse, L.main_cpu, L.parse,
+		        L.slot_wait, L.acquire, L.read_s, L.read_bytes / 1e9, L.copy_s, L.copy_bytes / 1e9, L.copy_mode,
+		        L.guess_s, L.worker_cpu, L.worker_wall);
+	}
 	if (range) {
 		range->stopped = S.stopped;
 		range->next = S.stopped ? UINT64_MAX : expect;
@@ -698,9 +904,25 @@ extern "C" int vc_scan_file_parallel(const char *path, int k, int block_bases, i
 	if (!path || !st || n_threads < 1) return VC_EINVAL;
 	vc_file_stats local = {0, 0, 0, 0.0};
 	const double t0 = mono_now();
+	struct stat sb;
+	if (stat(path, &sb) != 0) return VC_EIO;
+	if (!S_ISREG(sb.st_mode)) {   // a FIFO: read once, by the sequential reader (as vc_count_file)
+		VcFastqReader rd;
+		if (!rd.open(path)) return VC_EIO;
+		size_t nb = 0, nr = 0;
+		const int rc = vc_block_loop(rd, k, block_bases, [&](const char *q, size_t l) {
+			if (seq_out && nb + l <= seq_cap) memcpy(seq_out + nb, q, l);
+			if (lens_out && nr < lens_cap) lens_out[nr] = (uint32_t)l;
+			nb += l;
+			++nr;
+			return VC_OK;
+		}, local);
+		local.seconds = mono_now() - t0;
+		*st = local;
+		return rc;
+	}
 	const int fd = open(path, O_RDONLY);
 	if (fd < 0) return VC_EIO;
-	struct stat sb;
 	if (fstat(fd, &sb) != 0) {
 		close(fd);
 		return VC_EIO;
@@ -759,13 +981,14 @@ extern "C" int vc_scan_file_range(const char *path, int k, int block_bases, int 
 	vc_file_stats local = {0, 0, 0, 0.0};
 	*ri = vc_range_info{UINT64_MAX, UINT64_MAX, 0, 0, 1};
 	const double t0 = mono_now();
-	const int fd = open(path, O_RDONLY);
-	if (fd < 0) return VC_EIO;
 	struct stat sb;
+	if (stat(path, &sb) != 0) return VC_EIO;
+	const int fd = S_ISREG(sb.st_mode) ? open(path, O_RDONLY) : -1;   // a FIFO is opened once, below
+	if (S_ISREG(sb.st_mode) && fd < 0) return VC_EIO;
 	uint8_t magic[2] = {0, 0};
-	const bool reg = fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
+	const bool reg = fd >= 0 && fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
 	if (!reg || (pread_full(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b)) {
-		close(fd);   // not split (vc_count_file_range): the first range takes the whole file
+		if (fd >= 0) close(fd);   // not split (vc_count_file_range): the first range takes the whole file
 		int rc = VC_OK;
 		if (begin == 0) {
 			rc = vc_scan_file_parallel(path, k, block_bases, n_threads, piece_bytes, &local, seq_out, seq_cap,
@@ -802,5 +1025,16 @@ extern "C" uint64_t vc_ingest_profile(double *prof)
 		prof[5] = L.slot_wait;
 		prof[6] = L.acquire;
 	}
+	return L.pieces;
+}
+
+extern "C" uint64_t vc_ingest_profile_ex(double *prof, int n)
+{
+	const VcIngestProfile &L = vc_ingest_last;
+	const double v[VC_INGEST_PROFILE_FIELDS] = {
+		L.total, L.main_wait, L.submit, L.reparse, L.parse, L.slot_wait, L.acquire, L.read_s,
+		(double)L.read_bytes, L.copy_s, (double)L.copy_bytes, L.guess_s, L.worker_cpu, L.worker_wall,
+		L.main_cpu, (double)L.threads, (double)L.copy_mode};
+	for (int i = 0; prof && i < n && i < VC_INGEST_PROFILE_FIELDS; ++i) prof[i] = v[i];
 	return L.pieces;
 }

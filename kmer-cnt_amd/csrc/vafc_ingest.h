@@ -118,10 +118,17 @@ struct VcTextRange {
 // kernel launches), re-parsing mis-guessed pieces; worker thread-seconds
 // parsing, waiting for a slot the main thread has not released, and waiting
 // in the sink's acquire (the slot's previous copy still in flight).
+// The workers' parse splits further into the reads out of the source
+// (pread: the copy out of the page cache), the batched sequence copies into
+// the slots (VAFC_SLOT_COPY 1/2; 0 copies per read, untimed) and the record
+// guesses; their CPU seconds against their wall seconds tell descheduled
+// time (a CPU quota's throttling) from work.
 struct VcIngestProfile {
 	double total = 0, main_wait = 0, submit = 0, reparse = 0, parse = 0, slot_wait = 0, acquire = 0;
+	double read_s = 0, copy_s = 0, guess_s = 0, worker_cpu = 0, worker_wall = 0, main_cpu = 0;
+	uint64_t read_bytes = 0, copy_bytes = 0;
 	uint64_t pieces = 0;
-	int threads = 0;
+	int threads = 0, copy_mode = 0;
 };
 extern thread_local VcIngestProfile vc_ingest_last;
 

@@ -40,7 +40,7 @@ EXPORTS = (
     "vc_count_block", "vc_count_device", "vc_finish", "vc_reset", "vc_device_counts",
     "vc_bind_outputs", "vc_device_tally", "vc_stream", "vc_set_timing", "vc_kernel_ms",
     "vc_table_info", "vc_create_multi", "vc_shard_count", "vc_shard_info", "vc_count_file",
-    "vc_count_file_range", "vc_scan_file_range", "vc_ingest_profile", "vc_scan_file", "vc_scan_file_parallel",
+    "vc_count_file_range", "vc_scan_file_range", "vc_ingest_profile", "vc_ingest_profile_ex", "vc_scan_file", "vc_scan_file_parallel",
     "vc_scan_records", "vc_reserve_file_ingest",
     "vc_gz_inflate_parallel", "vc_gz_inflate_zlib", "vc_gz_crc32",
     "vc_fasta_load", "vc_fasta_count", "vc_fasta_name", "vc_fasta_seq", "vc_fasta_data", "vc_fasta_free",
@@ -134,6 +134,7 @@ def lib():
                                          C.c_uint64, C.POINTER(FileStats), C.POINTER(RangeInfo), P, C.c_size_t,
                                          P, C.c_size_t]),
         "vc_ingest_profile": (C.c_uint64, [P]),
+        "vc_ingest_profile_ex": (C.c_uint64, [P, C.c_int]),
         "vc_scan_file": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(FileStats), P, C.c_size_t,
                                    P, C.c_size_t]),
         "vc_scan_file_parallel": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_uint64,
@@ -573,15 +574,20 @@ def scan_file_range(fn: str, k: int, begin: int, end: int, block_size: int = 10_
 
 
 INGEST_PROFILE_KEYS = ("reader_s", "main_wait_s", "submit_s", "reparse_s", "parse_thread_s", "slot_wait_thread_s",
-                       "acquire_thread_s")
+                       "acquire_thread_s", "read_thread_s", "read_bytes", "copy_thread_s", "copy_bytes",
+                       "guess_thread_s", "worker_cpu_s", "worker_wall_s", "main_cpu_s", "threads", "copy_mode")
 
 
 def ingest_profile() -> dict:
-    """vc_ingest_profile: where this thread's last pass through the parallel
-    reader spent its time (seconds; *_thread_s summed over the workers)."""
-    out = np.zeros(7, np.float64)
-    n = lib().vc_ingest_profile(_ptr(out))
+    """vc_ingest_profile_ex: where this thread's last pass through the parallel
+    reader spent its time (seconds; *_thread_s summed over the workers; the
+    parse split into the reads out of the source, the batched slot copies and
+    the record guesses; worker CPU against wall seconds)."""
+    out = np.zeros(len(INGEST_PROFILE_KEYS), np.float64)
+    n = lib().vc_ingest_profile_ex(_ptr(out), len(out))
     d = {k: round(float(v), 4) for k, v in zip(INGEST_PROFILE_KEYS, out)}
+    for k in ("read_bytes", "copy_bytes", "threads", "copy_mode"):
+        d[k] = int(d[k])
     d["pieces"] = int(n)
     return d
 

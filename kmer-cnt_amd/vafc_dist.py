@@ -19,8 +19,10 @@ the path shards with no data-path collective:
   met a truncated record (a -2 ends a block, and the file's end -- the third
   empty block -- depends on the blocks before it).  The ranks exchange their
   (first, next, errs) with one all-gather per file; if the chain does not
-  hold, every rank restores its counts from before the file and rank 0
-  counts the file whole, which is exactly vc_count_file;
+  hold, every rank restores its counts from before the file and rank
+  i mod N counts file i whole, which is exactly vc_count_file.  Rank 0
+  decides up front which files are split and their sizes (one all-gather),
+  so every rank takes the same branch for every file;
 * gzip files (one deflate stream: no random access) are dealt whole, file
   i to rank i mod N;
 * the per-rank uint32 count vectors and the tallies (valid k-mers, bases,
@@ -273,17 +275,46 @@ def _khashl_capacity(n: int) -> int:
     return 1 << bits
 
 
+def file_plan(files, rank: int, world: int, coll_device):
+    """How each file is counted, decided by rank 0 and shared with one
+    all-gather before the first file, so that no rank can take another branch
+    (and another collective) for a file that changed meanwhile: [(split,
+    size)], split for a regular non-gzip file when world > 1, size its length
+    then (-1: rank 0 could not stat it; the file is dealt whole)."""
+    plan = []
+    for fn in files:
+        split = world > 1 and splittable(fn)
+        size = -1
+        if split:
+            try:
+                size = os.path.getsize(fn)
+            except OSError:
+                split = False
+        plan.append((1 if split else 0, size if split else NO_OFFSET))
+    if world == 1:
+        return [(bool(a), b) for a, b in plan]
+    flat = [x for ab in plan for x in ab] or [0]
+    rows = allgather_ints(flat, world, coll_device)
+    r0 = rows[0]
+    return [(bool(r0[2 * i]), int(r0[2 * i + 1])) for i in range(len(files))]
+
+
 def count_files(files, counter, o, rank, world, err, coll_device):
     """The reference's per-file loop (vaf-counter.c:644-650) over the ranks:
-    (ok, bases, seqs, fallbacks).  ok is False on every rank as soon as any
-    rank's counter failed."""
+    (ok, bases, seqs, fallbacks, per_file).  ok is False on every rank as soon
+    as any rank's counter failed.  per_file[i] = (opened, bases, seqs,
+    seconds) of file i over all ranks, for the -v line of count_fastq_kmers
+    (vaf-counter.c:573-578; rank 0 prints them after the loop)."""
     bases = seqs = fallbacks = 0
     ok = True
+    plan = file_plan(files, rank, world, coll_device)
+    mine = [[0, 0, 0, 0] for _ in files]   # this rank's (opened, bases, seqs, microseconds) per file
     for i, fn in enumerate(files):
         if rank == 0:
             err("[M::main] Processing %s...\n" % fn)
-        if world > 1 and splittable(fn):
-            size = os.path.getsize(fn)
+        split, size = plan[i]
+        t_file = time.time()
+        if split:
             begin, end = byte_range(size, rank, world)
             counter.save()
             failed = False
@@ -304,17 +335,20 @@ def count_files(files, counter, o, rank, world, err, coll_device):
             if chain_holds([r[:4] for r in rows]):
                 bases += b
                 seqs += s
+                mine[i] = [1, b, s, int(1e6 * (time.time() - t_file))]
                 continue
             # not an exact split (a truncated record, a mis-guessed boundary):
-            # rank 0 counts the file whole, the others forget their share
+            # every rank forgets its share and rank i mod N counts the file
+            # whole, so several such files spread over the ranks
             fallbacks += 1
             counter.restore()
-            if rank == 0:
+            if i % world == rank:
                 try:
                     good, b, s, _ = counter.count_range(fn, 0, NO_OFFSET, o["b"], o["t"])
                     if good:
                         bases += b
                         seqs += s
+                        mine[i] = [1, b, s, int(1e6 * (time.time() - t_file))]
                 except Exception as e:
                     err("Error: counting failed on %s (%s)\n" % (fn, e))
                     ok = False
@@ -330,7 +364,32 @@ def count_files(files, counter, o, rank, world, err, coll_device):
         if good:
             bases += b
             seqs += s
-    return ok, bases, seqs, fallbacks
+            mine[i] = [1, b, s, int(1e6 * (time.time() - t_file))]
+    # every rank reaches this point (a failure in a split file breaks every
+    # rank's loop together), so one all-gather gives rank 0 every file's totals
+    if world > 1 and files:
+        rows = allgather_ints([x for m in mine for x in m], world, coll_device)
+        per_file = []
+        for i in range(len(files)):
+            parts = [r[4 * i:4 * i + 4] for r in rows]
+            per_file.append((any(p[0] for p in parts), sum(p[1] for p in parts), sum(p[2] for p in parts),
+                             max(p[3] for p in parts) * 1e-6))
+    else:
+        per_file = [(bool(m[0]), m[1], m[2], m[3] * 1e-6) for m in mine]
+    return ok, bases, seqs, fallbacks, per_file
+
+
+def rank_device(local: int, local_world: int, n_dev: int, backend: str, rehearsal: bool):
+    """The GPU of local rank `local`: one per rank.  More ranks on this node
+    than visible GPUs is refused (None): RCCL refuses duplicate GPUs, and a
+    gloo run would silently put two ranks on one card under an N-GPU label.
+    An explicit gloo rehearsal (VAFC_DIST_BACKEND=gloo, VAFC_REHEARSAL=1)
+    wraps the ranks onto the GPUs there are."""
+    if n_dev >= 1 and local_world <= n_dev and local < n_dev:
+        return local
+    if rehearsal and backend == "gloo" and n_dev >= 1:
+        return local % n_dev
+    return None
 
 
 def run(argv, make_counter, rank: int = 0, world: int = 1, err=None, coll_device="cpu") -> int:
@@ -391,7 +450,12 @@ def run(argv, make_counter, rank: int = 0, world: int = 1, err=None, coll_device
         import torch.distributed as dist
         dist.barrier()
     t = time.time()
-    ok, bases, seqs, _ = count_files(files, counter, o, rank, world, err, coll_device)
+    ok, bases, seqs, _, per_file = count_files(files, counter, o, rank, world, err, coll_device)
+    if ok and o["v"] and rank == 0:
+        for fn, (opened, b, sq, sec) in zip(files, per_file):
+            if opened:   # count_fastq_kmers returns before its line for a file it cannot open
+                err("[V::count_fastq_kmers] Processed %s: %d sequences, %d bases in %.2f sec (%.2f Mbases/sec)\n"
+                    % (fn, sq, b, sec, b / sec / 1e6 if sec > 0 else 0.0))
     counts_t = None
     km = 0
     if ok:
@@ -476,7 +540,14 @@ def main(argv=None) -> int:
     import torch
     import torch.distributed as dist
     backend = os.environ.get("VAFC_DIST_BACKEND", "nccl")
-    local = local % max(torch.cuda.device_count(), 1)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    n_dev = torch.cuda.device_count()
+    dev = rank_device(local, local_world, n_dev, backend, os.environ.get("VAFC_REHEARSAL") == "1")
+    if dev is None:
+        sys.stderr.write("Error: local rank %d of %d but %d GPU(s) visible: one GPU per rank (a gloo rehearsal on "
+                         "fewer GPUs needs VAFC_DIST_BACKEND=gloo VAFC_REHEARSAL=1)\n" % (local, local_world, n_dev))
+        return 1
+    local = dev
     torch.cuda.set_device(local)
     if world > 1:
         if backend == "nccl":

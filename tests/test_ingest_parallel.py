@@ -228,3 +228,41 @@ def test_ranges_of_gzip_are_whole(tmp_path):
     st, ri, reads = vafc.scan_file_range(p, 3, 5, D.NO_OFFSET, with_reads=True)
     assert ri.whole == 1 and st.seqs == 0 and ri.first == D.NO_OFFSET
     assert not D.splittable(p)
+
+
+def _feed_fifo(fifo, data, result):
+    """Writer side of a named pipe: the whole text, then close; records an
+    EPIPE (the reader went away early) instead of raising."""
+    try:
+        with open(fifo, "wb") as w:
+            w.write(data)
+        result["ok"] = True
+    except BrokenPipeError:
+        result["ok"] = False
+
+
+@pytest.mark.parametrize("how", ["range", "parallel"])
+def test_fifo_is_opened_once(tmp_path, how):
+    """A named pipe is read by one open, as the reference's gzopen reads it
+    (vc_count_file_range opened the path, looked at it, closed it
+    and reopened it, so the writer could see its reader go away): the range
+    reader and the parallel reader take it whole through the sequential
+    reader, with the same reads as the regular file."""
+    import threading
+    import vafc
+    src = os.path.join(CASES, PLAIN[0])
+    data = open(src, "rb").read()
+    fifo = str(tmp_path / "in.fifo")
+    os.mkfifo(fifo)
+    res = {}
+    t = threading.Thread(target=_feed_fifo, args=(fifo, data, res))
+    t.start()
+    if how == "range":
+        st, ri, _ = vafc.scan_file_range(fifo, 5, 0, 1 << 40, 100, threads=3, piece_bytes=64)
+        assert ri.whole == 1
+    else:
+        st, _ = vafc.scan_file_parallel(fifo, 5, 100, threads=3, piece_bytes=64)
+    t.join(timeout=60)
+    assert res.get("ok") is True
+    st0, _ = vafc.scan_file(src, 5, 100)
+    assert (st.bases, st.seqs, st.blocks) == (st0.bases, st0.seqs, st0.blocks) and st0.seqs > 0

@@ -258,6 +258,17 @@ def test_dist_driver_matches_reference(name, world, counter, manifest, synth_dir
     inputs = [a for a in entry["argv"] if a.endswith((".fq", ".gz", ".fa"))]
     assert [ln.split("Processing ")[1][:-3] for ln in err.splitlines() if "Processing " in ln] == inputs
     assert "Ranks:" not in err
+    # count_fastq_kmers' -v line (vaf-counter.c:573-578): one per input that
+    # opens, in argv order, the files' sequences and bases adding up to the totals
+    from conftest import case_dir
+    proc = [ln for ln in err.splitlines() if ln.startswith("[V::count_fastq_kmers] Processed ")]
+    if "-v" in entry["argv"] and entry["exit"] == 0:
+        opened = [i for i in inputs if os.path.exists(os.path.join(case_dir(entry, synth_dir), i))]
+        assert [ln.split("Processed ")[1].split(": ")[0] for ln in proc] == opened, proc
+        assert sum(int(ln.split(": ")[1].split()[0]) for ln in proc) == stats["seqs"]
+        assert sum(int(ln.split(" sequences, ")[1].split()[0]) for ln in proc) == stats["bases"]
+    else:
+        assert not proc
     if counter == "oracle":
         if name in DIST_CLEAN:
             assert all(c["restores"] == 0 and c["ranges"] >= 1 for c in calls), calls

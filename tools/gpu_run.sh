@@ -47,7 +47,7 @@ bench)
   cut -c1-600 "$O/${TAG}_bench.json"
   ;;
 bench2)
-  VAFC_DIST_BACKEND=gloo timeout -k 10 900 python bench.py --gpus 2 "$@" > "$O/${TAG}_bench2.json" \
+  VAFC_DIST_BACKEND=gloo VAFC_REHEARSAL=1 timeout -k 10 900 python bench.py --gpus 2 "$@" > "$O/${TAG}_bench2.json" \
     2> "$O/${TAG}_bench2.err" || fail $? "$O/${TAG}_bench2.err"
   cut -c1-600 "$O/${TAG}_bench2.json"
   ;;
