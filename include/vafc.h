@@ -295,6 +295,67 @@ int64_t vc_gz_inflate_zlib(const char *path, uint8_t *out, uint64_t cap);
 /* Host-only: zlib-compatible CRC-32 of p[0..n) continuing from crc (the
  * inflater's member check; PCLMULQDQ folding where the CPU has it). */
 uint32_t vc_gz_crc32(uint32_t crc, const uint8_t *p, uint64_t n);
+/* zlib's crc32_combine: the CRC-32 of A then B from crc(A), crc(B), len(B). */
+uint32_t vc_gz_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
+
+/* One gzip file over several ranks (round 6, kmer-cnt_amd/vafc_dist.py; the
+ * reference reads it with one gzread, vaf-counter.c:557, kseq.h:74-85).
+ * Rank r's share is the text of the deflate blocks from the first dynamic
+ * block starting at or after byte A_r of the file up to the first dynamic
+ * block starting at or after A_{r+1} (A_0 = 0: the stream's start).
+ *
+ * 1. vc_gz_share_scan: each rank decodes its share speculatively without
+ *    the history before it and reports where the share starts and ends (bit
+ *    offsets), its text length, and its last 32 KiB of text as symbols
+ *    (window_sym, 32768 entries: a byte value < 256, or 0x8000 | i for byte i
+ *    of the unknown 32 KiB before the share).  ok = 0: the share could not be
+ *    decoded without that history (the caller counts the file whole).
+ * 2. The shares chain iff each share's start_bit equals the previous
+ *    (non-empty) share's end_bit; the 32 KiB before share r+1 is share r's
+ *    window_sym with every 0x8000 | i replaced by byte i of the 32 KiB before
+ *    share r (share 0's history is empty).
+ * 3. vc_count_gz_share: the share's reads, counted from start_bit with that
+ *    window: the records whose header lies in the share's text, the block
+ *    loop starting afresh at the first, as vc_count_file_range does for a
+ *    byte range of a plain file.  ri.first / ri.next are offsets in the
+ *    share's own text / the next share's text, so consecutive shares are
+ *    exact under the same chain rule (first == previous next, no -2).  crc
+ *    reports the CRC-32 accounting of the share: members wholly inside are
+ *    checked (crc_error), the member open at the share's start closes at its
+ *    first member end (head_*, to be checked by the caller with the previous
+ *    shares' tails) and the one open at its end is the tail. */
+typedef struct {
+	uint64_t start_bit;   /* UINT64_MAX: no dynamic block starts in the share's bytes (an empty share) */
+	uint64_t end_bit;     /* UINT64_MAX: the stream ended inside the share */
+	uint64_t text_len;    /* bytes of text from start_bit to end_bit */
+	uint32_t ok;
+	uint32_t ended;
+} vc_gz_share_info;
+int vc_gz_share_scan(const char *path, uint64_t begin, uint64_t end, int n_threads, uint64_t chunk_bytes,
+                     vc_gz_share_info *out, uint16_t *window_sym);
+
+typedef struct {
+	uint32_t events;            /* member ends inside the share */
+	uint32_t head_crc;          /* CRC-32 of the share's text up to its first member end */
+	uint64_t head_len;
+	uint32_t head_expect_crc;   /* that member's trailer (CRC-32, ISIZE) */
+	uint32_t head_expect_isize;
+	uint32_t tail_crc;          /* from the last member end (or the share's start) to the share's end */
+	uint64_t tail_len;
+	uint32_t crc_error;         /* a member wholly inside the share failed its check */
+	uint32_t complete;          /* the accounting reached the share's end */
+} vc_gz_share_crc;
+/* first_share: the stream's start (start_bit and window unused).  Counts like
+ * vc_count_file_range (NULL ri/crc not allowed); VC_EIO if the file cannot be
+ * opened as gzip. */
+int vc_count_gz_share(vc_ctx *ctx, const char *path, int first_share, uint64_t start_bit, const uint8_t *window,
+                      uint64_t text_len, int block_bases, int n_threads, vc_file_stats *st, vc_range_info *ri,
+                      vc_gz_share_crc *crc);
+/* Host-only: the same reader without a device (accepted reads copied out
+ * while they fit, as vc_scan_file_range). */
+int vc_scan_gz_share(const char *path, int k, int first_share, uint64_t start_bit, const uint8_t *window,
+                     uint64_t text_len, int block_bases, int n_threads, vc_file_stats *st, vc_range_info *ri,
+                     vc_gz_share_crc *crc, uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out, size_t lens_cap);
 
 /* Host-only: the kseq_read return value of every record until -1 (inclusive),
  * written while they fit; returns the number of calls made, or VC_EIO. */

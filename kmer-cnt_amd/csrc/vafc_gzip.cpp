@@ -4,6 +4,7 @@
 // zlib (the reference's gzread, pinned by the system package) remains the
 // decoder of record for every chunk whose speculative decode is not used.
 #include "vafc_gzip.h"
+#include "vafc.h"
 #include "vafc_affinity.h"
 
 #include <fcntl.h>
@@ -707,6 +708,8 @@ struct Chunk {
 	Out out;
 	bool busy = false;                // slot in use (decoding, or held until resolved)
 	bool decoded = false;
+	bool known = false;               // starts at the stream's first block (empty history, no search)
+	bool end_dynamic = false;         // share scans: stop only at a dynamic block (one a search can find)
 	std::unique_ptr<Tables> tab{new Tables};
 };
 
@@ -739,8 +742,11 @@ bool decode_blocks(const uint8_t *p, uint64_t n, BitIn &in, Chunk &C, bool first
 	for (;;) {
 		const uint64_t at = in.bitpos();
 		if (at >= C.nom_b && !first) {
-			C.end = at;
-			return o.finish();
+			in.refill();
+			if (!C.end_dynamic || ((in.buf >> 1) & 3) == 2) {
+				C.end = at;
+				return o.finish();
+			}
 		}
 		first = false;
 		in.refill();
@@ -834,7 +840,7 @@ void decode_chunk(const uint8_t *p, uint64_t n, uint64_t first_bit, Chunk &C)
 	C.events.clear();
 	Out &o = C.out;
 	BitIn in;
-	if (C.index == 0) {   // the stream's start: known (empty) history
+	if (C.known) {   // the stream's start: known (empty) history
 		o.reset(true);
 		C.start = (int64_t)first_bit;
 		in.init(p, n, first_bit);
@@ -1059,10 +1065,33 @@ void piece_crcs(Piece &P)
 
 } // namespace
 
+// How a VcGzParallel covers the stream (vafc_gzip.h, shares of one stream).
+struct GzShareOpts {
+	bool scan = false;                // vc_gzp_scan_share
+	uint64_t begin = 0, end = UINT64_MAX;   // scan: the share's nominal bytes
+	bool first_share = true;          // stream: from the stream's start
+	uint64_t start_bit = 0;           // stream, later shares: the share's first block
+	const uint8_t *window = nullptr;  // stream, later shares: the 32 KiB before it
+	uint64_t text_len = UINT64_MAX;   // stream: the share's text (CRC accounting)
+};
+
 class VcGzParallel {
 public:
 	~VcGzParallel() { shutdown(); }
-	bool start(const char *path, int threads, uint64_t chunk_bytes);
+	bool start(const char *path, int threads, uint64_t chunk_bytes, const GzShareOpts *so = nullptr);
+	// scan mode: wait for the scan's result
+	void scan_result(VcGzShare *sh, uint16_t *wsym)
+	{
+		std::unique_lock<std::mutex> lk(mu_);
+		cv_.wait(lk, [&] { return seq_done_; });
+		*sh = share_;
+		if (wsym) memcpy(wsym, wsym_.data(), WSIZE * sizeof(uint16_t));
+	}
+	void share_crc(VcGzShareCrc *out)
+	{
+		std::lock_guard<std::mutex> lk(mu_);
+		*out = scrc_;
+	}
 	int64_t read(uint8_t *dst, size_t n);
 	int64_t span(const uint8_t **out, size_t maxn, void **hold = nullptr);
 	void release(void *hold);
@@ -1100,9 +1129,30 @@ private:
 	uint32_t mcrc_ = 0;
 	uint64_t mlen_ = 0;
 	bool done_ = false;
+	// shares (vafc_gzip.h)
+	bool known_start_ = true;         // chunk 0 starts at the stream's first block
+	bool scan_ = false;               // scan mode: symbols of the share's last 32 KiB, no text
+	uint64_t last_bit_ = 0;           // the chunks cover [first_bit_, last_bit_)
+	VcGzShare share_;
+	std::vector<uint16_t> wsym_ = std::vector<uint16_t>(WSIZE);
+	uint64_t share_len_ = UINT64_MAX; // stream mode: CRC accounting stops at this text offset
+	uint64_t pbase_ = 0;              // text offset of cur_'s first byte
+	bool crc_stopped_ = false;
+	VcGzShareCrc scrc_;
 
 	void worker();
 	void sequencer();
+	void scan_sequencer();
+	void share_cut(const Piece &P, size_t cut);   // the CRC accounting reaches the share's end
+	void stream_done_crc()   // the stream ended before the share's end: what is open is the tail
+	{
+		if (share_len_ == UINT64_MAX || crc_stopped_) return;
+		std::lock_guard<std::mutex> lk(mu_);
+		scrc_.tail_crc = mcrc_;
+		scrc_.tail_len = mlen_;
+		scrc_.complete = stats.crc_error ? 0u : 1u;
+		crc_stopped_ = true;
+	}
 	bool fallback(uint64_t &expect, uint64_t nom_b, bool &ended);
 	Piece *new_piece();
 	bool push_piece(std::unique_ptr<Piece> P);   // waits for queue space; false on stop
@@ -1203,8 +1253,10 @@ void VcGzParallel::worker()
 		dec->busy = true;
 		dec->decoded = false;
 		dec->index = j;
+		dec->known = j == 0 && known_start_;
+		dec->end_dynamic = scan_;
 		dec->nom_a = first_bit_ + j * chunk_bits_;
-		dec->nom_b = j + 1 == nchunks_ ? n_ * 8 : first_bit_ + (j + 1) * chunk_bits_;
+		dec->nom_b = j + 1 == nchunks_ ? last_bit_ : first_bit_ + (j + 1) * chunk_bits_;
 		lk.unlock();
 		decode_chunk(p_, n_, first_bit_, *dec);
 		lk.lock();
@@ -1388,7 +1440,95 @@ void VcGzParallel::sequencer()
 	cv_.notify_all();
 }
 
-bool VcGzParallel::start(const char *path, int threads, uint64_t chunk_bytes)
+// Scan mode: the chunks of the share in order, each taken only where it
+// begins at the previous one's end (no zlib fallback: the history before the
+// share is unknown); the share's last 32 KiB kept as symbols that name bytes
+// of the window before the share (vafc_gzip.h).
+void VcGzParallel::scan_sequencer()
+{
+	for (uint32_t i = 0; i < WSIZE; ++i) wsym_[i] = (uint16_t)(MARK | i);
+	std::vector<uint16_t> tail(WSIZE);
+	uint64_t expect = known_start_ ? first_bit_ : UINT64_MAX;
+	if (known_start_) share_.start_bit = first_bit_;
+	else member_text_ = WSIZE;        // a member open before the share: its history is the full window
+	bool ok = true, ended = false;
+	uint64_t len = 0;
+	for (uint64_t j = 0; j < nchunks_ && ok && !ended; ++j) {
+		Chunk *C = slots_[j % slots_.size()].get();
+		{
+			std::unique_lock<std::mutex> lk(mu_);
+			cv_.wait(lk, [&] { return stop_ || (C->index == j && C->decoded); });
+			if (stop_) {
+				ok = false;
+				break;
+			}
+		}
+		auto release = [&]() {
+			std::lock_guard<std::mutex> lk(mu_);
+			C->busy = false;
+			cv_.notify_all();
+		};
+		if (expect == UINT64_MAX) {   // the share's first block: in the first chunk that found one
+			if (C->start < 0) {
+				release();
+				continue;
+			}
+			expect = (uint64_t)C->start;
+			share_.start_bit = expect;
+		}
+		if (expect >= C->nom_b) {
+			release();
+			continue;
+		}
+		const uint64_t have = std::min<uint64_t>(member_text_, WSIZE);
+		if (!(C->ok && C->start >= 0 && (uint64_t)C->start == expect && C->out.min_mark >= WSIZE - have)) {
+			ok = false;
+			release();
+			break;
+		}
+		const Out &o = C->out;
+		const size_t n = o.nt;
+		const size_t tn = std::min<size_t>(n, WSIZE);
+		for (size_t i = 0; i < tn; ++i) {
+			const size_t x = n - tn + i;
+			const uint16_t v = x >= o.res ? (uint16_t)o.t[x] : o.s[x];
+			tail[i] = v < 256 ? v : wsym_[v & (WSIZE - 1)];
+		}
+		if (tn == WSIZE) {
+			memcpy(wsym_.data(), tail.data(), WSIZE * sizeof(uint16_t));
+		} else if (tn) {
+			memmove(wsym_.data(), wsym_.data() + tn, (WSIZE - tn) * sizeof(uint16_t));
+			memcpy(wsym_.data() + WSIZE - tn, tail.data(), tn * sizeof(uint16_t));
+		}
+		len += n;
+		member_text_ = C->events.empty() ? member_text_ + n : n - C->events.back().off;
+		expect = C->end;
+		ended = C->stream_end;
+		release();
+	}
+	std::lock_guard<std::mutex> lk(mu_);
+	share_.ok = ok;
+	share_.text_len = share_.start_bit == UINT64_MAX ? 0 : len;
+	share_.end_bit = ended || share_.start_bit == UINT64_MAX ? UINT64_MAX : expect;
+	seq_done_ = true;
+	cv_.notify_all();
+}
+
+// The reader has delivered the share's last byte, at offset `cut` of piece P
+// (inside the segment that starts at seg_a_): the CRC of the member still open
+// there is the share's tail.
+void VcGzParallel::share_cut(const Piece &P, size_t cut)
+{
+	const size_t part = cut - seg_a_;
+	const uint32_t c = part ? vc_crc32(0, P.text + seg_a_, part) : 0;
+	std::lock_guard<std::mutex> lk(mu_);
+	scrc_.tail_crc = (uint32_t)crc32_combine(mcrc_, c, (z_off_t)part);
+	scrc_.tail_len = mlen_ + part;
+	scrc_.complete = 1;
+	crc_stopped_ = true;
+}
+
+bool VcGzParallel::start(const char *path, int threads, uint64_t chunk_bytes, const GzShareOpts *so)
 {
 	fd_ = open(path, O_RDONLY);
 	if (fd_ < 0) return false;
@@ -1402,14 +1542,37 @@ bool VcGzParallel::start(const char *path, int threads, uint64_t chunk_bytes)
 	const int64_t d = member_header(p_, n_, 0);
 	if (d < 0) return false;
 	first_bit_ = (uint64_t)d * 8;
+	last_bit_ = n_ * 8;
+	if (so && so->scan) {
+		scan_ = true;
+		if (so->begin > 0) {   // a later share: its first block is searched for
+			known_start_ = false;
+			first_bit_ = std::max<uint64_t>(first_bit_, std::min<uint64_t>(so->begin, n_) * 8);
+		}
+		if (so->end < n_) last_bit_ = std::max<uint64_t>(first_bit_, so->end * 8);
+		if (first_bit_ >= last_bit_) {   // nothing of the stream in the share
+			share_.ok = true;
+			seq_done_ = true;
+			return true;
+		}
+	} else if (so) {
+		share_len_ = so->text_len;
+		if (!so->first_share) {
+			if (so->start_bit >= n_ * 8 || !so->window) return false;
+			known_start_ = false;
+			first_bit_ = so->start_bit;
+			memcpy(window_.data(), so->window, WSIZE);
+			member_text_ = WSIZE;
+		}
+	}
 	if (threads < 1) threads = 1;
 	if (chunk_bytes == 0) {   // about four chunks per worker, 1..4 MiB each
-		chunk_bytes = n_ / (4 * (uint64_t)threads);
+		chunk_bytes = (last_bit_ - first_bit_) / 8 / (4 * (uint64_t)threads);
 		chunk_bytes = std::max<uint64_t>((uint64_t)1 << 20, std::min<uint64_t>((uint64_t)4 << 20, chunk_bytes));
 	}
 	if (chunk_bytes < 1024) chunk_bytes = 1024;
 	chunk_bits_ = chunk_bytes * 8;
-	nchunks_ = (n_ * 8 - first_bit_ + chunk_bits_ - 1) / chunk_bits_;
+	nchunks_ = (last_bit_ - first_bit_ + chunk_bits_ - 1) / chunk_bits_;
 	if (nchunks_ == 0) nchunks_ = 1;
 	stats.chunks = nchunks_;
 	if (threads < 1) threads = 1;
@@ -1427,7 +1590,8 @@ bool VcGzParallel::start(const char *path, int threads, uint64_t chunk_bytes)
 		});
 	seq_ = std::thread([this, cpus] {
 		vc_affinity_bind(cpus);
-		sequencer();
+		if (scan_) scan_sequencer();
+		else sequencer();
 	});
 	return true;
 }
@@ -1440,6 +1604,7 @@ int64_t VcGzParallel::span(const uint8_t **out, size_t maxn, void **hold)
 		if (done_ || maxn == 0) return 0;
 		if (cur_ && spent_) {   // release the piece the previous span pointed into
 			const bool last = cur_->stream_end;
+			pbase_ += cur_->n;
 			{
 				std::lock_guard<std::mutex> lk(mu_);
 				std::unique_ptr<Piece> P = std::move(pieces_.front());
@@ -1451,6 +1616,7 @@ int64_t VcGzParallel::span(const uint8_t **out, size_t maxn, void **hold)
 			cur_ = nullptr;
 			if (last) {
 				done_ = true;
+				stream_done_crc();
 				return 0;
 			}
 		}
@@ -1461,6 +1627,8 @@ int64_t VcGzParallel::span(const uint8_t **out, size_t maxn, void **hold)
 			prof_rdwait_us += (uint64_t)((gz_now() - w0) * 1e6);
 			if (pieces_.empty()) {
 				done_ = true;
+				lk.unlock();
+				stream_done_crc();
 				return 0;
 			}
 			cur_ = pieces_.front().get();
@@ -1471,6 +1639,11 @@ int64_t VcGzParallel::span(const uint8_t **out, size_t maxn, void **hold)
 		const size_t lim = ev_ < P.events.size() ? (size_t)P.events[ev_].off : P.n;
 		if (rd_ < lim) {
 			const size_t take = std::min(maxn, lim - rd_);
+			// a share ends inside this segment: its tail is accounted as soon as
+			// its last byte goes out (the reader may stop soon after)
+			if (!crc_stopped_ && share_len_ != UINT64_MAX && pbase_ + lim > share_len_ &&
+			    pbase_ + rd_ + take >= share_len_)
+				share_cut(P, (size_t)(share_len_ - pbase_));
 			*out = P.text + rd_;
 			if (hold) {
 				std::lock_guard<std::mutex> lk(mu_);
@@ -1482,21 +1655,56 @@ int64_t VcGzParallel::span(const uint8_t **out, size_t maxn, void **hold)
 			return (int64_t)take;
 		}
 		// a segment is complete: its CRC joins the member's
+		if (crc_stopped_) {   // past a share's end: another rank accounts for the rest
+			seg_a_ = lim;
+			if (ev_ < P.events.size()) {
+				++ev_;
+				continue;
+			}
+			spent_ = true;
+			continue;
+		}
+		if (share_len_ != UINT64_MAX && pbase_ + lim > share_len_) {   // the share ends inside this segment
+			share_cut(P, (size_t)(share_len_ - pbase_));
+			continue;
+		}
 		const size_t seg = lim - seg_a_;
 		mcrc_ = (uint32_t)crc32_combine(mcrc_, P.seg_crc[ev_], (z_off_t)seg);
 		mlen_ += seg;
 		seg_a_ = lim;
 		if (ev_ < P.events.size()) {
 			const Event &e = P.events[ev_];
-			if (mcrc_ != e.crc || (uint32_t)mlen_ != e.isize) {   // gzread stops at a failed check
-				stats.crc_error = 1;
-				done_ = true;
-				return 0;
+			if (share_len_ != UINT64_MAX && scrc_.events == 0) {
+				// a share's first member end: the member may have begun in an
+				// earlier share, so its check is the caller's (vafc_gzip.h)
+				std::lock_guard<std::mutex> lk(mu_);
+				scrc_.head_crc = mcrc_;
+				scrc_.head_len = mlen_;
+				scrc_.head_expect_crc = e.crc;
+				scrc_.head_expect_isize = e.isize;
+				scrc_.events = 1;
+			} else {
+				if (mcrc_ != e.crc || (uint32_t)mlen_ != e.isize) {   // gzread stops at a failed check
+					std::lock_guard<std::mutex> lk(mu_);
+					stats.crc_error = 1;
+					scrc_.crc_error = 1;
+					done_ = true;
+					return 0;
+				}
+				if (share_len_ != UINT64_MAX) {
+					std::lock_guard<std::mutex> lk(mu_);
+					++scrc_.events;
+				}
 			}
 			++stats.members;
 			mcrc_ = 0;
 			mlen_ = 0;
 			++ev_;
+			if (share_len_ != UINT64_MAX && pbase_ + lim == share_len_) share_cut(P, lim);   // a member ends the share
+			continue;
+		}
+		if (share_len_ != UINT64_MAX && pbase_ + lim == share_len_) {
+			share_cut(P, lim);
 			continue;
 		}
 		spent_ = true;
@@ -1575,6 +1783,41 @@ void vc_gzp_stats(VcGzParallel *g, VcGzStats *st) { g->get_stats(st); }
 
 void vc_gzp_close(VcGzParallel *g) { delete g; }
 
+bool vc_gzp_scan_share(const char *path, int threads, uint64_t chunk_bytes, uint64_t begin, uint64_t end,
+                       VcGzShare *sh, uint16_t *window_sym)
+{
+	GzShareOpts so;
+	so.scan = true;
+	so.begin = begin;
+	so.end = end;
+	VcGzParallel *g = new VcGzParallel;
+	if (!g->start(path, threads, chunk_bytes, &so)) {
+		delete g;
+		return false;
+	}
+	g->scan_result(sh, window_sym);
+	delete g;
+	return true;
+}
+
+VcGzParallel *vc_gzp_open_share(const char *path, int threads, uint64_t chunk_bytes, bool first_share,
+                                uint64_t start_bit, const uint8_t *window, uint64_t text_len)
+{
+	GzShareOpts so;
+	so.first_share = first_share;
+	so.start_bit = start_bit;
+	so.window = window;
+	so.text_len = text_len;
+	VcGzParallel *g = new VcGzParallel;
+	if (!g->start(path, threads, chunk_bytes, &so)) {
+		delete g;
+		return nullptr;
+	}
+	return g;
+}
+
+void vc_gzp_share_crc(VcGzParallel *g, VcGzShareCrc *out) { g->share_crc(out); }
+
 // ---------------------------------------------------------------------------
 // host-only test hooks (C ABI): the whole decompressed stream, parallel and
 // through gzread, into caller buffers
@@ -1623,3 +1866,23 @@ extern "C" int64_t vc_gz_inflate_zlib(const char *path, uint8_t *out, uint64_t c
 }
 
 extern "C" uint32_t vc_gz_crc32(uint32_t crc, const uint8_t *p, uint64_t n) { return vc_crc32(crc, p, n); }
+
+extern "C" uint32_t vc_gz_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2)
+{
+	return (uint32_t)crc32_combine64(crc1, crc2, (z_off64_t)len2);
+}
+
+extern "C" int vc_gz_share_scan(const char *path, uint64_t begin, uint64_t end, int n_threads, uint64_t chunk_bytes,
+                                vc_gz_share_info *out, uint16_t *window_sym)
+{
+	if (!path || !out || end <= begin) return VC_EINVAL;
+	VcGzShare sh;
+	if (!vc_gzp_scan_share(path, n_threads < 1 ? 1 : n_threads, chunk_bytes, begin, end, &sh, window_sym))
+		return VC_EIO;
+	out->start_bit = sh.start_bit;
+	out->end_bit = sh.end_bit;
+	out->text_len = sh.text_len;
+	out->ok = sh.ok ? 1u : 0u;
+	out->ended = sh.start_bit != UINT64_MAX && sh.end_bit == UINT64_MAX ? 1u : 0u;
+	return VC_OK;
+}

@@ -49,6 +49,62 @@ class VcGzParallel;
 // or it cannot be mapped: the caller then reads it with gzread.  chunk_bytes
 // 0: about four chunks per worker, 1 to 4 MiB of compressed input each.
 VcGzParallel *vc_gzp_open(const char *path, int threads, uint64_t chunk_bytes);
+
+// ---------------------------------------------------------------------------
+// Shares of one gzip stream over several ranks (round 6; the torchrun driver,
+// kmer-cnt_amd/vafc_dist.py).  Rank r's share is the text of the deflate
+// blocks from the first dynamic block that starts at or after byte A_r of the
+// file to the first dynamic block that starts at or after A_{r+1}.
+//
+//   1. scan (vc_gzp_scan_share): the share's chunks are decoded speculatively
+//      as always, and instead of text the sequencer keeps the share's last
+//      32 KiB as symbols: a literal byte, or MARK | i for byte i of the
+//      unknown 32 KiB before the share (markers of each chunk are mapped
+//      through the previous chunk's symbols, so they all name that one
+//      window).  A chunk that cannot be taken (a wrong start, a stored or
+//      fixed block at the boundary, corrupt data) fails the scan: without the
+//      history zlib cannot redo it, and the caller counts the file whole.
+//   2. the ranks exchange (start, end, text length, last-32 KiB symbols); the
+//      window before share r+1 is share r's symbols resolved against the
+//      window before share r, so every window follows from rank 0's, whose
+//      history is known (empty).
+//   3. stream (vc_gzp_open_share): each rank inflates from its start bit with
+//      its now known window, through the ordinary sequencer (zlib fallback
+//      included), and on past its share's end as far as the reader asks (the
+//      last record of a share ends in the next one).  CRC-32 accounting covers
+//      the share only: the member that was open at the share's start and the
+//      one still open at its end are reported as partial CRCs for the caller
+//      to combine across ranks (vc_gz_crc32_combine); members wholly inside
+//      are checked as gzread checks them.
+// ---------------------------------------------------------------------------
+struct VcGzShare {
+	uint64_t start_bit = UINT64_MAX;   // UINT64_MAX: no dynamic block starts in the share's bytes
+	uint64_t end_bit = UINT64_MAX;     // UINT64_MAX: the stream ended inside the share
+	uint64_t text_len = 0;             // bytes of text from start_bit to end_bit
+	bool ok = false;                   // every chunk of the share decoded and chained
+};
+// begin/end: the share's nominal bytes [A_r, A_{r+1}) of the compressed file
+// (begin 0: the stream's first member, whose history is known).  window_sym
+// (WSIZE = 32768 entries): the share's last 32 KiB of text as symbols.  false
+// if the file cannot be opened as gzip.
+bool vc_gzp_scan_share(const char *path, int threads, uint64_t chunk_bytes, uint64_t begin, uint64_t end,
+                       VcGzShare *sh, uint16_t *window_sym);
+
+struct VcGzShareCrc {
+	uint32_t events = 0;               // member ends met inside the share
+	uint32_t head_crc = 0;             // CRC-32 of the share's text up to its first member end
+	uint64_t head_len = 0;
+	uint32_t head_expect_crc = 0, head_expect_isize = 0;   // that member's trailer
+	uint32_t tail_crc = 0;             // after the last member end (the whole share if none)
+	uint64_t tail_len = 0;
+	uint32_t crc_error = 0;            // a member wholly inside the share failed its check
+	uint32_t complete = 0;             // the accounting reached the share's end (or the stream's)
+};
+// Stream from start_bit with the 32 KiB `window` before it (first_share: the
+// stream's start, window unused); text_len bounds the CRC accounting.
+VcGzParallel *vc_gzp_open_share(const char *path, int threads, uint64_t chunk_bytes, bool first_share,
+                                uint64_t start_bit, const uint8_t *window, uint64_t text_len);
+void vc_gzp_share_crc(VcGzParallel *g, VcGzShareCrc *out);
 // Next bytes of the decompressed stream, in order: > 0 bytes, 0 at the end.
 int64_t vc_gzp_read(VcGzParallel *g, uint8_t *dst, size_t n);
 // The same without a copy: up to `max` next bytes at *p, valid until the next

@@ -19,6 +19,7 @@
 #include <fcntl.h>
 #include <limits.h>
 #include <math.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <stdio.h>
@@ -234,6 +235,9 @@ struct Slot {
 	hipEvent_t done = nullptr;
 	hipEvent_t copied = nullptr;  // parallel reader: the slot's H2D copies (copy stream) are done
 	bool pending = false;
+	void *map = nullptr;          // one registered mapping holds h_seq, h_offs, h_lens (slot_alloc_mapped)
+	size_t map_len = 0;
+	bool d_one = false;           // d_offs, d_lens point into d_seq's allocation
 };
 
 } // namespace
@@ -484,12 +488,22 @@ fail:
 
 static void free_slot(Slot &s)
 {
-	if (s.h_seq) (void)hipHostFree(s.h_seq);
-	if (s.h_offs) (void)hipHostFree(s.h_offs);
-	if (s.h_lens) (void)hipHostFree(s.h_lens);
+	if (s.map) {
+		(void)hipHostUnregister(s.map);
+		munmap(s.map, s.map_len);
+	} else {
+		if (s.h_seq) (void)hipHostFree(s.h_seq);
+		if (s.h_offs) (void)hipHostFree(s.h_offs);
+		if (s.h_lens) (void)hipHostFree(s.h_lens);
+	}
 	if (s.d_seq) (void)hipFree(s.d_seq);
-	if (s.d_offs) (void)hipFree(s.d_offs);
-	if (s.d_lens) (void)hipFree(s.d_lens);
+	if (!s.d_one) {
+		if (s.d_offs) (void)hipFree(s.d_offs);
+		if (s.d_lens) (void)hipFree(s.d_lens);
+	}
+	s.map = nullptr;
+	s.map_len = 0;
+	s.d_one = false;
 	s.h_seq = nullptr;
 	s.h_offs = nullptr;
 	s.h_lens = nullptr;
@@ -1209,6 +1223,7 @@ public:
 		HIPCK(hipSetDevice(sh->dev));
 		Slot n;
 		n.done = s.done;
+		n.copied = s.copied;
 		if (hipHostMalloc(&n.h_seq, bytes, hipHostMallocDefault) != hipSuccess ||
 		    hipHostMalloc(&n.h_offs, reads * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
 		    hipHostMalloc(&n.h_lens, reads * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
@@ -1307,9 +1322,65 @@ static int reserve_ingest(vc_ctx *c, int threads, bool alloc)
 // One slot's buffers.  FASTQ: at most half of a piece's records' text is
 // sequence (the quality line is as long); FASTA and long records grow the slot.
 static size_t ingest_slot_bytes(uint64_t piece) { return (size_t)piece / 2 + ((size_t)256 << 10); }
+
+// A slot's pinned buffers as one anonymous mapping on transparent huge pages,
+// touched and registered with hipHostRegister, and its device buffers as one
+// allocation: pinning 32 slots of a 16 MB piece took 0.018 s this way against
+// 0.041-0.057 s as three hipHostMalloc + three hipMalloc each, at the same
+// 52 GB/s H2D (tools/pin_probe.hip, profiles/r06b_pin_probe.log).  The CLI pins
+// its slots inside the counting timer, as the reference allocates its block
+// buffers inside it.  VAFC_PIN=malloc keeps hipHostMalloc (A/B).
+static int slot_alloc_mapped(Slot &s, size_t bytes, size_t reads)
+{
+	const size_t huge = (size_t)2 << 20;
+	const size_t ob = (bytes + 63) / 64 * 64, lb = ob + reads * sizeof(uint64_t);
+	const size_t need = lb + reads * sizeof(uint32_t);
+	const size_t len = (need + huge - 1) / huge * huge;
+	void *m = mmap(nullptr, len + huge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+	if (m == MAP_FAILED) return VC_ENOMEM;
+	// the 2 MB-aligned part only (the slack before and after goes back)
+	uint8_t *a = (uint8_t *)(((uintptr_t)m + huge - 1) / huge * huge);
+	if (a > (uint8_t *)m) munmap(m, (size_t)(a - (uint8_t *)m));
+	const size_t tail = (size_t)((uint8_t *)m + len + huge - (a + len));
+	if (tail) munmap(a + len, tail);
+	madvise(a, len, MADV_HUGEPAGE);
+	for (size_t i = 0; i < len; i += 4096) a[i] = 0;   // fault the pages in (huge pages where granted)
+	if (hipHostRegister(a, len, hipHostRegisterDefault) != hipSuccess) {
+		(void)hipGetLastError();
+		munmap(a, len);
+		return VC_EHIP;
+	}
+	uint8_t *d = nullptr;
+	if (hipMalloc(&d, need) != hipSuccess) {
+		(void)hipGetLastError();
+		(void)hipHostUnregister(a);
+		munmap(a, len);
+		return VC_EHIP;
+	}
+	s.map = a;
+	s.map_len = len;
+	s.h_seq = a;
+	s.h_offs = (uint64_t *)(a + ob);
+	s.h_lens = (uint32_t *)(a + lb);
+	s.d_seq = d;
+	s.d_offs = (uint64_t *)(d + ob);
+	s.d_lens = (uint32_t *)(d + lb);
+	s.d_one = true;
+	s.cap_bytes = bytes;
+	s.cap_reads = reads;
+	return VC_OK;
+}
+
 static int ingest_slot_alloc(Slot &s, uint64_t piece)
 {
-	return slot_reserve(s, ingest_slot_bytes(piece), (size_t)piece / 256 + 4096);
+	static const bool use_malloc = getenv("VAFC_PIN") && !strcmp(getenv("VAFC_PIN"), "malloc");
+	if (use_malloc) return slot_reserve(s, ingest_slot_bytes(piece), (size_t)piece / 256 + 4096);
+	const size_t bytes = ingest_slot_bytes(piece), reads = (size_t)piece / 256 + 4096;
+	if (bytes <= s.cap_bytes && reads <= s.cap_reads) return VC_OK;
+	if (s.pending) HIPCK(hipEventSynchronize(s.done));
+	s.pending = false;
+	free_slot(s);
+	return slot_alloc_mapped(s, bytes + bytes / 4 + 4096, reads + reads / 4 + 1024);
 }
 
 // alloc = false: only the slot records and their events; each slot's buffers
@@ -1541,6 +1612,55 @@ extern "C" int vc_count_file_range(vc_ctx *c, const char *path, uint64_t begin, 
 	close(fd);
 	if (rc == VC_OK) rc = sync_shards(c);
 	*ri = vc_range_info{R.first, R.next, R.errs, R.stopped ? 1u : 0u, 0u};
+	local.seconds = wall_now() - t0;
+	if (st) *st = local;
+	return rc;
+}
+
+// One share of a gzip file (include/vafc.h, vafc_gzip.h): the inflater from
+// the share's first block with its known window, the parallel reader over the
+// share's text as a range (plus the previous byte, for the first guess).
+extern "C" int vc_count_gz_share(vc_ctx *c, const char *path, int first_share, uint64_t start_bit,
+                                 const uint8_t *window, uint64_t text_len, int block_bases, int n_threads,
+                                 vc_file_stats *st, vc_range_info *ri, vc_gz_share_crc *crc)
+{
+	if (!c || !path || !ri || !crc || text_len == 0 || (!first_share && !window)) return VC_EINVAL;
+	vc_file_stats local = {0, 0, 0, 0.0};
+	*ri = vc_range_info{UINT64_MAX, UINT64_MAX, 0, 0, 0};
+	memset(crc, 0, sizeof *crc);
+	const double t0 = wall_now();
+	HIPCK(hipSetDevice(c->dev));
+	const int fmt = vc_gz_text_format(path);
+	if (fmt < 0) return VC_EINVAL;
+	const int t = clamp_threads(n_threads);
+	VcAffinityScope placement(gpu_cpus(c, vc_gz_inflate_threads(t) + vc_gz_parse_threads(t) + 2));
+	const char *ce = getenv("VAFC_GZ_CHUNK");   // test knob: compressed bytes per chunk
+	VcGzParallel *g = vc_gzp_open_share(path, vc_gz_inflate_threads(t), ce ? (uint64_t)atoll(ce) : 0,
+	                                    first_share != 0, start_bit, window, text_len);
+	if (!g) return VC_EIO;
+	const int parsers = vc_gz_parse_threads(t);
+	int rc = reserve_ingest(c, parsers, false);
+	VcTextRange R;
+	const size_t np = first_share ? 0 : 1;
+	if (rc >= 0) {
+		const int slots = rc;
+		const char *pe = getenv("VAFC_INGEST_PIECE");          // test knob: piece size in bytes
+		const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : VC_PIECE_BYTES;
+		DeviceSink sink(c, piece);
+		R.begin = np;
+		R.end = np + text_len;
+		R.format = fmt;
+		rc = vc_ingest_gzip_share(g, first_share ? nullptr : window + 32767, np, c->k, block_bases, parsers, slots,
+		                          piece, (uint64_t)(slots + 2) * piece * 2, sink, local, &R);
+	}
+	VcGzShareCrc sc;
+	vc_gzp_share_crc(g, &sc);
+	vc_gzp_close(g);
+	if (rc == VC_OK) rc = sync_shards(c);
+	*ri = vc_range_info{R.first == UINT64_MAX ? UINT64_MAX : R.first - np,
+	                    R.next == UINT64_MAX ? UINT64_MAX : R.next - np - text_len, R.errs, R.stopped ? 1u : 0u, 0u};
+	*crc = vc_gz_share_crc{sc.events, sc.head_crc, sc.head_len, sc.head_expect_crc, sc.head_expect_isize,
+	                       sc.tail_crc, sc.tail_len, sc.crc_error, sc.complete};
 	local.seconds = wall_now() - t0;
 	if (st) *st = local;
 	return rc;

@@ -239,8 +239,17 @@ private:
 // more (a record longer than the window must still be read).
 class GzSource : public VcIngestSource {
 public:
-	GzSource(VcGzParallel *g, uint64_t window) : g_(g), window_(window)
+	GzSource(VcGzParallel *g, uint64_t window, const uint8_t *prefix = nullptr, size_t np = 0) : g_(g), window_(window)
 	{
+		if (np) {   // bytes that precede the stream in the text (a gzip share's previous byte)
+			Block *b = new Block;
+			uint8_t *c = (uint8_t *)malloc(np);
+			memcpy(c, prefix, np);
+			b->p = c;
+			b->len = np;
+			blocks_.push_back(b);
+			end_ = np;
+		}
 		pump_ = std::thread([this, cpus = vc_affinity_get()] {
 			vc_affinity_bind(cpus);
 			pump();
@@ -606,7 +615,9 @@ int vc_ingest_text(VcIngestSource &src, int k, int block_bases, int threads, int
 	}
 	if (!src.longer_than(0)) return VC_OK;   // empty input: three empty blocks, nothing counted
 	bool fasta = false;
-	{
+	if (range && range->format >= 0) {
+		fasta = range->format == 1;
+	} else {
 		VcFastqReader rd;
 		if (!rd.open_src(&src, 0, (size_t)1 << 16)) return VC_ENOMEM;
 		const int64_t h = rd.peek_header();
@@ -819,6 +830,34 @@ int vc_ingest_gzip(VcGzParallel *g, int k, int block_bases, int threads, int slo
 	return vc_ingest_text(src, k, block_bases, threads, slots, piece_bytes, sink, st);
 }
 
+int vc_ingest_gzip_share(VcGzParallel *g, const uint8_t *prefix, size_t np, int k, int block_bases, int threads,
+                         int slots, uint64_t piece_bytes, uint64_t window_bytes, VcIngestSink &sink, vc_file_stats &st,
+                         VcTextRange *range)
+{
+	GzSource src(g, window_bytes, prefix, np);
+	return vc_ingest_text(src, k, block_bases, threads, slots, piece_bytes, sink, st, range);
+}
+
+int vc_gz_text_format(const char *path)
+{
+	gzFile f = gzopen(path, "r");
+	if (!f) return -1;
+	uint8_t buf[1 << 16];
+	int fmt = -1;
+	for (size_t seen = 0; fmt < 0 && seen < ((size_t)1 << 20);) {
+		const int n = gzread(f, buf, sizeof buf);
+		if (n <= 0) break;
+		for (int i = 0; i < n; ++i)
+			if (buf[i] == '>' || buf[i] == '@') {
+				fmt = buf[i] == '>' ? 1 : 0;
+				break;
+			}
+		seen += (size_t)n;
+	}
+	gzclose(f);
+	return fmt;
+}
+
 // ---------------------------------------------------------------------------
 // host-only hook: the parallel ingest without a device (tests, ingest speed)
 // ---------------------------------------------------------------------------
@@ -1008,6 +1047,45 @@ extern "C" int vc_scan_file_range(const char *path, int k, int block_bases, int 
 	                               local, &R);
 	close(fd);
 	*ri = vc_range_info{R.first, R.next, R.errs, R.stopped ? 1u : 0u, 0u};
+	local.seconds = mono_now() - t0;
+	*st = local;
+	return rc;
+}
+
+extern "C" int vc_scan_gz_share(const char *path, int k, int first_share, uint64_t start_bit, const uint8_t *window,
+                                uint64_t text_len, int block_bases, int n_threads, vc_file_stats *st,
+                                vc_range_info *ri, vc_gz_share_crc *crc, uint8_t *seq_out, size_t seq_cap,
+                                uint32_t *lens_out, size_t lens_cap)
+{
+	if (!path || !st || !ri || !crc || n_threads < 1 || text_len == 0 || (!first_share && !window)) return VC_EINVAL;
+	vc_file_stats local = {0, 0, 0, 0.0};
+	*ri = vc_range_info{UINT64_MAX, UINT64_MAX, 0, 0, 0};
+	memset(crc, 0, sizeof *crc);
+	const double t0 = mono_now();
+	const int fmt = vc_gz_text_format(path);
+	if (fmt < 0) return VC_EINVAL;
+	const char *ce = getenv("VAFC_GZ_CHUNK");   // test knob: compressed bytes per chunk
+	VcGzParallel *g = vc_gzp_open_share(path, vc_gz_inflate_threads(n_threads), ce ? (uint64_t)atoll(ce) : 0,
+	                                    first_share != 0, start_bit, window, text_len);
+	if (!g) return VC_EIO;
+	const char *pe = getenv("VAFC_INGEST_PIECE");
+	const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : ((uint64_t)16 << 20);
+	const int parsers = vc_gz_parse_threads(n_threads);
+	HostSink sink(parsers + 2, piece, seq_out, seq_cap, lens_out, lens_cap);
+	const size_t np = first_share ? 0 : 1;
+	VcTextRange R;
+	R.begin = np;
+	R.end = np + text_len;
+	R.format = fmt;
+	const int rc = vc_ingest_gzip_share(g, first_share ? nullptr : window + 32767, np, k, block_bases, parsers,
+	                                    parsers + 2, piece, (uint64_t)(parsers + 4) * piece * 2, sink, local, &R);
+	VcGzShareCrc c;
+	vc_gzp_share_crc(g, &c);
+	vc_gzp_close(g);
+	*ri = vc_range_info{R.first == UINT64_MAX ? UINT64_MAX : R.first - np,
+	                    R.next == UINT64_MAX ? UINT64_MAX : R.next - np - text_len, R.errs, R.stopped ? 1u : 0u, 0u};
+	*crc = vc_gz_share_crc{c.events, c.head_crc, c.head_len, c.head_expect_crc, c.head_expect_isize, c.tail_crc,
+	                       c.tail_len, c.crc_error, c.complete};
 	local.seconds = mono_now() - t0;
 	*st = local;
 	return rc;

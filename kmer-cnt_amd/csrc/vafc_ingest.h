@@ -110,6 +110,7 @@ struct VcTextRange {
 	uint64_t begin = 0, end = UINT64_MAX;
 	uint64_t first = 0, next = UINT64_MAX, errs = 0;
 	bool stopped = false;
+	int format = -1;   // 1 FASTA, 0 FASTQ, -1: from the text's first header (a gzip share starts mid-stream)
 };
 
 // Where the last vc_ingest_text pass of the calling thread spent its time
@@ -167,5 +168,15 @@ inline int vc_gz_inflate_threads(int threads)
 }
 int vc_ingest_gzip(VcGzParallel *g, int k, int block_bases, int threads, int slots, uint64_t piece_bytes,
                    uint64_t window_bytes, VcIngestSink &sink, vc_file_stats &st);
+// One share of a gzip stream (vafc_gzip.h, vc_gzp_open_share): the text is
+// prefix[0..np) (the last byte before the share, so that the first piece's
+// guess sees whether the share starts at a line start) followed by the
+// share's stream; range covers [np, np + text_len).
+int vc_ingest_gzip_share(VcGzParallel *g, const uint8_t *prefix, size_t np, int k, int block_bases, int threads,
+                         int slots, uint64_t piece_bytes, uint64_t window_bytes, VcIngestSink &sink, vc_file_stats &st,
+                         VcTextRange *range);
+// FASTA (1) or FASTQ (0) by the first '>' or '@' of a gzip file's text (the
+// first kseq_read's scan, kseq.h:197-201), -1 if none in its first MiB.
+int vc_gz_text_format(const char *path);
 
 #endif

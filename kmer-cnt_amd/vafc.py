@@ -42,7 +42,8 @@ EXPORTS = (
     "vc_table_info", "vc_create_multi", "vc_shard_count", "vc_shard_info", "vc_count_file",
     "vc_count_file_range", "vc_scan_file_range", "vc_ingest_profile", "vc_ingest_profile_ex", "vc_scan_file", "vc_scan_file_parallel",
     "vc_scan_records", "vc_reserve_file_ingest",
-    "vc_gz_inflate_parallel", "vc_gz_inflate_zlib", "vc_gz_crc32",
+    "vc_gz_inflate_parallel", "vc_gz_inflate_zlib", "vc_gz_crc32", "vc_gz_crc32_combine",
+    "vc_gz_share_scan", "vc_count_gz_share", "vc_scan_gz_share",
     "vc_fasta_load", "vc_fasta_count", "vc_fasta_name", "vc_fasta_seq", "vc_fasta_data", "vc_fasta_free",
     "vc_count_candidates", "vc_set_nt4_decode",
     "vc_kc_create", "vc_kc_set_partition", "vc_kc_slots", "vc_kc_histogram", "vc_kc_histogram2",
@@ -75,7 +76,24 @@ class RangeInfo(C.Structure):
                 ("stopped", C.c_uint32), ("whole", C.c_uint32)]
 
 
+class GzShareInfo(C.Structure):
+    """vc_gz_share_info: one rank's share of a gzip stream (vc_gz_share_scan)."""
+    _fields_ = [("start_bit", C.c_uint64), ("end_bit", C.c_uint64), ("text_len", C.c_uint64),
+                ("ok", C.c_uint32), ("ended", C.c_uint32)]
+
+
+class GzShareCrc(C.Structure):
+    """vc_gz_share_crc: the CRC-32 accounting of one share (vc_count_gz_share)."""
+    _fields_ = [("events", C.c_uint32), ("head_crc", C.c_uint32), ("head_len", C.c_uint64),
+                ("head_expect_crc", C.c_uint32), ("head_expect_isize", C.c_uint32), ("tail_crc", C.c_uint32),
+                ("tail_len", C.c_uint64), ("crc_error", C.c_uint32), ("complete", C.c_uint32)]
+
+    def as_dict(self):
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
 NO_OFFSET = (1 << 64) - 1   # vc_range_info's UINT64_MAX
+GZ_WSIZE = 32768            # deflate's window; symbols 0x8000 | i name byte i of the window before a share
 
 
 _lib = None
@@ -143,6 +161,14 @@ def lib():
         "vc_gz_inflate_parallel": (C.c_int64, [C.c_char_p, C.c_int, C.c_uint64, P, C.c_uint64, P]),
         "vc_gz_inflate_zlib": (C.c_int64, [C.c_char_p, P, C.c_uint64]),
         "vc_gz_crc32": (C.c_uint32, [C.c_uint32, P, C.c_uint64]),
+        "vc_gz_crc32_combine": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint64]),
+        "vc_gz_share_scan": (C.c_int, [C.c_char_p, C.c_uint64, C.c_uint64, C.c_int, C.c_uint64,
+                                       C.POINTER(GzShareInfo), P]),
+        "vc_count_gz_share": (C.c_int, [P, C.c_char_p, C.c_int, C.c_uint64, P, C.c_uint64, C.c_int, C.c_int,
+                                        C.POINTER(FileStats), C.POINTER(RangeInfo), C.POINTER(GzShareCrc)]),
+        "vc_scan_gz_share": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_uint64, P, C.c_uint64, C.c_int, C.c_int,
+                                       C.POINTER(FileStats), C.POINTER(RangeInfo), C.POINTER(GzShareCrc),
+                                       P, C.c_size_t, P, C.c_size_t]),
         "vc_reserve_file_ingest": (C.c_int, [P, C.c_int]),
         "vc_fasta_load": (C.c_int, [C.c_char_p, C.POINTER(P)]),
         "vc_fasta_count": (C.c_int, [P]),
@@ -381,6 +407,20 @@ class KmerMap:
         _ck(rc, "vc_count_file(%s)" % fn)
         return st
 
+    def count_gz_share(self, fn: str, first_share: bool, start_bit: int, window, text_len: int,
+                       block_size: int = 10_000_000, n_thread: int = 4):
+        """One rank's share of a gzip file (vc_count_gz_share): (FileStats,
+        RangeInfo in share coordinates, CRC accounting dict)."""
+        st, ri, cr = FileStats(), RangeInfo(), GzShareCrc()
+        w = None if window is None else np.ascontiguousarray(window, dtype=np.uint8)
+        rc = lib().vc_count_gz_share(self._h, fn.encode(), 1 if first_share else 0, start_bit,
+                                     None if w is None else _ptr(w), text_len, block_size, n_thread,
+                                     C.byref(st), C.byref(ri), C.byref(cr))
+        if rc == VC_EIO:
+            raise FileNotFoundError(fn)
+        _ck(rc, "vc_count_gz_share(%s)" % fn)
+        return st, ri, cr.as_dict()
+
     def count_file_range(self, fn: str, begin: int, end: int, block_size: int = 10_000_000,
                          n_thread: int = 4):
         """One rank's byte range [begin, end) of a file (vc_count_file_range):
@@ -571,6 +611,58 @@ def scan_file_range(fn: str, k: int, begin: int, end: int, block_size: int = 10_
         raise FileNotFoundError(fn)
     _ck(rc, "vc_scan_file_range")
     return st, ri, reads
+
+
+def gz_share_scan(fn: str, begin: int, end: int, threads: int = 4, chunk_bytes: int = 0):
+    """vc_gz_share_scan: (GzShareInfo as a dict, the share's last 32 KiB as
+    uint16 symbols)."""
+    info = GzShareInfo()
+    wsym = np.zeros(GZ_WSIZE, np.uint16)
+    rc = lib().vc_gz_share_scan(fn.encode(), begin, min(end, NO_OFFSET), threads, chunk_bytes, C.byref(info),
+                                _ptr(wsym))
+    if rc == VC_EIO:
+        raise FileNotFoundError(fn)
+    _ck(rc, "vc_gz_share_scan(%s)" % fn)
+    return {f: int(getattr(info, f)) for f, _ in info._fields_}, wsym
+
+
+def gz_window_after(wsym: np.ndarray, before: np.ndarray) -> np.ndarray:
+    """The 32 KiB of text after a share from its symbols and the 32 KiB
+    before it (include/vafc.h: 0x8000 | i is byte i of `before`)."""
+    w = np.asarray(wsym, dtype=np.uint16)
+    b = np.asarray(before, dtype=np.uint8)
+    return np.where(w < 256, w, b[w & (GZ_WSIZE - 1)]).astype(np.uint8)
+
+
+def gz_crc32_combine(crc1: int, crc2: int, len2: int) -> int:
+    return int(lib().vc_gz_crc32_combine(crc1, crc2, len2))
+
+
+def scan_gz_share(fn: str, k: int, first_share: bool, start_bit: int, window, text_len: int,
+                  block_size: int = 10_000_000, threads: int = 4, with_reads: bool = False, cap: int = 0):
+    """Host-only vc_scan_gz_share: (FileStats, RangeInfo, CRC dict, reads or None)."""
+    st, ri, cr = FileStats(), RangeInfo(), GzShareCrc()
+    w = None if window is None else np.ascontiguousarray(window, dtype=np.uint8)
+    seq = lens = None
+    if with_reads:
+        n = max(cap or 2 * text_len + 4096, 64)
+        seq = np.zeros(n, np.uint8)
+        lens = np.zeros(max(n // 2, 16), np.uint32)
+    rc = lib().vc_scan_gz_share(fn.encode(), k, 1 if first_share else 0, start_bit, None if w is None else _ptr(w),
+                                text_len, block_size, threads, C.byref(st), C.byref(ri), C.byref(cr),
+                                None if seq is None else _ptr(seq), 0 if seq is None else seq.size,
+                                None if lens is None else _ptr(lens), 0 if lens is None else lens.size)
+    if rc == VC_EIO:
+        raise FileNotFoundError(fn)
+    _ck(rc, "vc_scan_gz_share(%s)" % fn)
+    reads = None
+    if with_reads:
+        reads, pos = [], 0
+        for i in range(int(st.seqs)):
+            m = int(lens[i])
+            reads.append(seq[pos:pos + m].tobytes())
+            pos += m
+    return st, ri, cr.as_dict(), reads
 
 
 INGEST_PROFILE_KEYS = ("reader_s", "main_wait_s", "submit_s", "reparse_s", "parse_thread_s", "slot_wait_thread_s",

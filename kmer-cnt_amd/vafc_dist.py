@@ -23,8 +23,17 @@ the path shards with no data-path collective:
   i mod N counts file i whole, which is exactly vc_count_file.  Rank 0
   decides up front which files are split and their sizes (one all-gather),
   so every rank takes the same branch for every file;
-* gzip files (one deflate stream: no random access) are dealt whole, file
-  i to rank i mod N;
+* a gzip file is split into shares of its deflate stream (round 6,
+  vafc_gzip.h): rank r decodes the blocks from the first dynamic block at or
+  after byte A_r of the file without the history before them and keeps its
+  last 32 KiB as symbols naming bytes of that unknown window; one all-gather
+  gives every rank the windows (each follows from the one before, rank 0's
+  history being empty), and every rank then counts its share's records from
+  its known window.  The ranges chain as for plain files, and the members'
+  CRC-32 checks are combined across the shares; anything else (a share that
+  cannot be decoded blind, a failed check) falls back to rank i mod N
+  counting file i whole.  Files that are neither are dealt whole, file i to
+  rank i mod N;
 * the per-rank uint32 count vectors and the tallies (valid k-mers, bases,
   sequences) are summed with ONE all-reduce each -- RCCL over xGMI with the
   "nccl" backend, gloo on CPU -- and rank 0 writes the .vaf and the -v report.
@@ -92,6 +101,77 @@ def splittable(fn: str) -> bool:
         return False
 
 
+def gz_file(fn: str) -> bool:
+    """A regular gzip file (split into shares of its deflate stream)."""
+    try:
+        if not os.path.isfile(fn):
+            return False
+        with open(fn, "rb") as f:
+            return f.read(2) == b"\x1f\x8b"
+    except OSError:
+        return False
+
+
+def gz_shares_chain(rows) -> bool:
+    """rows[r] = (start_bit, end_bit, text_len, ok, ended, ...) of rank r's
+    share scan (vc_gz_share_scan): the shares cover the stream exactly iff
+    every scan is ok, the first non-empty share is rank 0's, each non-empty
+    share starts at the previous non-empty share's end, and the last one ends
+    the stream (include/vafc.h)."""
+    if not rows or any(int(r[3]) != 1 for r in rows):
+        return False
+    ne = [r for r in rows if int(r[0]) != NO_OFFSET]
+    if not ne or ne[0] is not rows[0]:
+        return False
+    for prev, cur in zip(ne, ne[1:]):
+        if int(cur[0]) != int(prev[1]) or int(prev[4]) != 0:
+            return False
+    return int(ne[-1][4]) == 1
+
+
+def gz_windows(rows, wsyms):
+    """The 32 KiB of text before each rank's share: share 0's history is
+    empty; the window after a share is its symbols resolved against the
+    window before it (vafc.gz_window_after).  None for empty shares."""
+    import vafc
+    out = [None] * len(rows)
+    before = np.zeros(vafc.GZ_WSIZE, np.uint8)
+    prev = None
+    for r, row in enumerate(rows):
+        if int(row[0]) == NO_OFFSET:
+            continue
+        if prev is not None:
+            before = vafc.gz_window_after(wsyms[prev], before)
+        out[r] = before
+        prev = r
+    return out
+
+
+def gz_crc_chain(crcs, combine) -> bool:
+    """The CRC-32 accounting of the non-empty shares in order (dicts of
+    vc_gz_share_crc): no member inside a share failed, every share's first
+    member end checks with the tails of the shares before it
+    (combine = zlib's crc32_combine), and the stream's last member closed.
+    gzread checks the same members in one pass (vaf-counter.c:557)."""
+    carry_crc, carry_len = 0, 0
+    for c in crcs:
+        if c["crc_error"] or not c["complete"]:
+            return False
+        if c["events"] > 0:
+            crc = combine(carry_crc, c["head_crc"], c["head_len"])
+            if crc != c["head_expect_crc"] or (carry_len + c["head_len"]) & 0xFFFFFFFF != c["head_expect_isize"]:
+                return False
+            carry_crc, carry_len = c["tail_crc"], c["tail_len"]
+        else:
+            carry_crc = combine(carry_crc, c["tail_crc"], c["tail_len"])
+            carry_len += c["tail_len"]
+    return carry_len == 0
+
+
+GZ_CRC_FIELDS = ("events", "head_crc", "head_len", "head_expect_crc", "head_expect_isize", "tail_crc", "tail_len",
+                 "crc_error", "complete")
+
+
 def chain_holds(infos) -> bool:
     """infos[r] = (first, next, errs, stopped) of rank r's range, in rank order:
     the ranges counted exactly the file's reads iff no range met a truncated
@@ -144,6 +224,17 @@ def allreduce_max(value: float, device="cpu", group=None) -> float:
     return float(t.item())
 
 
+def allgather_u16(a: np.ndarray, world: int, device="cpu"):
+    """[rank 0's array, rank 1's, ...] for equal-length uint16 arrays."""
+    import torch
+    import torch.distributed as dist
+    # as int32 (gloo's all-gather has no 16-bit types)
+    t = torch.from_numpy(np.asarray(a, dtype=np.uint16).astype(np.int32)).to(device)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.cpu().numpy().astype(np.uint16) for o in out]
+
+
 def allgather_ints(values, world: int, device="cpu"):
     """[values of rank 0, values of rank 1, ...]: one all-gather of a few
     integers per rank (uint64 offsets travel as their int64 bit pattern)."""
@@ -174,6 +265,13 @@ class RankCounter:
         whose header lies in [first, end) (vafc.h vc_count_file_range); ok
         False if the file cannot be opened (skipped silently, as the reference
         does, vaf-counter.c:557).  begin = 0, end = NO_OFFSET: the whole file."""
+        raise NotImplementedError
+
+    def count_gz_share(self, fn: str, first_share: bool, start_bit: int, window, text_len: int, block: int,
+                       threads: int):
+        """(ok, bases, seqs, (first, next, errs, stopped), crc dict) of one
+        share of a gzip file (vafc.h vc_count_gz_share): first / next in share
+        coordinates; ok False if the file cannot be opened."""
         raise NotImplementedError
 
     def save(self):
@@ -225,6 +323,13 @@ class HipRankCounter(RankCounter):
         except FileNotFoundError:
             return False, 0, 0, (NO_OFFSET, NO_OFFSET, 0, 0)
         return True, st.bases, st.seqs, (ri.first, ri.next, ri.errs, ri.stopped)
+
+    def count_gz_share(self, fn, first_share, start_bit, window, text_len, block, threads):
+        try:
+            st, ri, crc = self.map.count_gz_share(fn, first_share, start_bit, window, text_len, block, threads)
+        except FileNotFoundError:
+            return False, 0, 0, (NO_OFFSET, NO_OFFSET, 0, 0), None
+        return True, st.bases, st.seqs, (ri.first, ri.next, ri.errs, ri.stopped), crc
 
     def save(self):
         # count_file_range returns after the map's stream is synchronised, so
@@ -278,25 +383,26 @@ def _khashl_capacity(n: int) -> int:
 def file_plan(files, rank: int, world: int, coll_device):
     """How each file is counted, decided by rank 0 and shared with one
     all-gather before the first file, so that no rank can take another branch
-    (and another collective) for a file that changed meanwhile: [(split,
-    size)], split for a regular non-gzip file when world > 1, size its length
-    then (-1: rank 0 could not stat it; the file is dealt whole)."""
+    (and another collective) for a file that changed meanwhile: [(kind,
+    size)] with kind 1 for a regular plain file split into byte ranges, 2 for
+    a regular gzip file split into shares of its stream (world > 1), 0 for a
+    file dealt whole; size the file's length for kinds 1 and 2."""
     plan = []
     for fn in files:
-        split = world > 1 and splittable(fn)
+        kind = (1 if splittable(fn) else (2 if gz_file(fn) else 0)) if world > 1 else 0
         size = -1
-        if split:
+        if kind:
             try:
                 size = os.path.getsize(fn)
             except OSError:
-                split = False
-        plan.append((1 if split else 0, size if split else NO_OFFSET))
+                kind = 0
+        plan.append((kind, size if kind else NO_OFFSET))
     if world == 1:
-        return [(bool(a), b) for a, b in plan]
+        return [(a, b) for a, b in plan]
     flat = [x for ab in plan for x in ab] or [0]
     rows = allgather_ints(flat, world, coll_device)
     r0 = rows[0]
-    return [(bool(r0[2 * i]), int(r0[2 * i + 1])) for i in range(len(files))]
+    return [(int(r0[2 * i]), int(r0[2 * i + 1])) for i in range(len(files))]
 
 
 def count_files(files, counter, o, rank, world, err, coll_device):
@@ -312,9 +418,22 @@ def count_files(files, counter, o, rank, world, err, coll_device):
     for i, fn in enumerate(files):
         if rank == 0:
             err("[M::main] Processing %s...\n" % fn)
-        split, size = plan[i]
+        kind, size = plan[i]
         t_file = time.time()
-        if split:
+        if kind == 2:
+            res = _count_gz_shares(fn, i, size, counter, o, rank, world, err, coll_device)
+            if res is None:        # a rank failed inside a collective step: every rank stops
+                ok = False
+                break
+            good, b, s, fell, local_ok = res
+            fallbacks += fell
+            ok = ok and local_ok
+            bases += b
+            seqs += s
+            if good:
+                mine[i] = [1, b, s, int(1e6 * (time.time() - t_file))]
+            continue
+        if kind == 1:
             begin, end = byte_range(size, rank, world)
             counter.save()
             failed = False
@@ -377,6 +496,71 @@ def count_files(files, counter, o, rank, world, err, coll_device):
     else:
         per_file = [(bool(m[0]), m[1], m[2], m[3] * 1e-6) for m in mine]
     return ok, bases, seqs, fallbacks, per_file
+
+
+def _count_gz_shares(fn, i, size, counter, o, rank, world, err, coll_device):
+    """File i, a gzip file, over the ranks (include/vafc.h, vafc_gzip.h):
+    every rank scans its share of the stream, the shares' windows follow from
+    one all-gather, every rank counts its share, and the ranges and CRC-32
+    accounting are checked as one chain.  Anything that does not chain (a
+    share that cannot be decoded blind, a record split wrongly, a member that
+    fails its check) is counted whole by rank i mod N instead, which is
+    exactly vc_count_file.  Returns (opened, bases, seqs, fallbacks, ok) of
+    this rank (ok False: its whole-file count failed; the other ranks go on, as
+    for a file dealt whole), or None when a rank failed during the shares (all
+    ranks stop)."""
+    import vafc
+    begin, end = byte_range(size, rank, world)
+    failed = False
+    info = {"start_bit": NO_OFFSET, "end_bit": NO_OFFSET, "text_len": 0, "ok": 1, "ended": 0}
+    wsym = np.zeros(vafc.GZ_WSIZE, np.uint16)
+    try:
+        if end > begin:
+            info, wsym = vafc.gz_share_scan(fn, begin, end, threads=o["t"])
+    except FileNotFoundError:
+        info["ok"] = 0
+    except Exception as e:
+        err("Error: counting failed on %s (%s)\n" % (fn, e))
+        failed = True
+    rows = allgather_ints([info["start_bit"], info["end_bit"], info["text_len"], info["ok"], info["ended"],
+                           1 if failed else 0], world, coll_device)
+    if any(r[5] for r in rows):
+        return None
+    wsyms = allgather_u16(wsym, world, coll_device)
+
+    def whole():
+        if i % world != rank:
+            return False, 0, 0, 1, True
+        try:
+            good, b, s, _ = counter.count_range(fn, 0, NO_OFFSET, o["b"], o["t"])
+        except Exception as e:
+            err("Error: counting failed on %s (%s)\n" % (fn, e))
+            return False, 0, 0, 1, False
+        return (True, b, s, 1, True) if good else (False, 0, 0, 1, True)
+
+    if not gz_shares_chain(rows):
+        return whole()
+    windows = gz_windows(rows, wsyms)
+    counter.save()
+    good, b, s, rinfo, crc = True, 0, 0, (EMPTY_RANGE, EMPTY_RANGE, 0, 0), None
+    if int(rows[rank][0]) != NO_OFFSET:
+        try:
+            good, b, s, rinfo, crc = counter.count_gz_share(fn, rank == 0, int(rows[rank][0]), windows[rank],
+                                                            int(rows[rank][2]), o["b"], o["t"])
+        except Exception as e:
+            err("Error: counting failed on %s (%s)\n" % (fn, e))
+            failed = True
+    cvals = [int((crc or {}).get(f, 0)) for f in GZ_CRC_FIELDS]
+    res = allgather_ints(list(rinfo) + [1 if good else 0, 1 if failed else 0] + cvals, world, coll_device)
+    if any(r[5] for r in res):
+        return None
+    nonempty = [r for r in range(world) if int(rows[r][0]) != NO_OFFSET]
+    crcs = [dict(zip(GZ_CRC_FIELDS, (int(x) for x in res[r][6:]))) for r in nonempty]
+    if all(res[r][4] for r in nonempty) and chain_holds([res[r][:4] for r in range(world)]) and \
+            gz_crc_chain(crcs, vafc.gz_crc32_combine):
+        return good, b, s, 0, True
+    counter.restore()
+    return whole()
 
 
 def rank_device(local: int, local_world: int, n_dev: int, backend: str, rehearsal: bool):

@@ -67,6 +67,8 @@ def synth_dir(tmp_path_factory, manifest):
     with open(os.path.join(d, "c1_10k.fq"), "rb") as f, \
             gzip.open(os.path.join(d, "c1_10k.fq.gz"), "wb", compresslevel=1) as g:
         g.write(f.read())
+    import gz_variants
+    gz_variants.make(d)
     for fn, want in manifest["synth"].items():
         with open(os.path.join(d, fn), "rb") as f:
             assert hashlib.md5(f.read()).hexdigest() == want, "synthetic generator drifted: " + fn

@@ -136,10 +136,13 @@ def test_cli_option_parsing_mirror():
 # --------------------------------------------------------------------------
 
 DIST_CASES = ["pe_k31", "c1_plumbing_k21", "c1_plumbing_k21_gz", "c1_k21_b1", "missing_file", "multiline_k21",
-              "edge_crlf_k21", "pat_edge_k31", "truncated", "empty_reads", "mal_gbbbgbbbg_b1", "mal_bg", "pal_k16"]
+              "edge_crlf_k21", "pat_edge_k31", "truncated", "empty_reads", "mal_gbbbgbbbg_b1", "mal_bg", "pal_k16",
+              "edge_gz", "gz_multi_k21", "gz_trailing_k21", "gz_mixed_k21"]
 # cases whose every file is well formed and plain: the byte ranges must chain
 # (no fallback to a whole-file recount)
 DIST_CLEAN = {"pe_k31", "c1_plumbing_k21", "c1_k21_b1", "pal_k16"}
+# well-formed gzip (and plain) files: shares of the stream, no whole-file count
+DIST_GZ_CLEAN = {"c1_plumbing_k21_gz", "edge_gz", "gz_multi_k21", "gz_trailing_k21", "gz_mixed_k21"}
 
 
 def _driver_rank(rank, world, port, argv, cwd, out_json, counter):
@@ -153,7 +156,7 @@ def _driver_rank(rank, world, port, argv, cwd, out_json, counter):
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     os.chdir(cwd)
     lines = []
-    calls = {"ranges": 0, "whole": 0, "restores": 0}
+    calls = {"ranges": 0, "whole": 0, "restores": 0, "gz_shares": 0}
 
     class OracleRankCounter(D.RankCounter):     # CPU stand-in for the per-GPU counter (test infrastructure)
         """The oracle counts what the product's host-only range reader
@@ -190,6 +193,23 @@ def _driver_rank(rank, world, port, argv, cwd, out_json, counter):
                 self.counts[:2 * self.n] += c
                 self.km += km
             return True, st.bases, st.seqs, (ri.first, ri.next, ri.errs, ri.stopped)
+
+        def count_gz_share(self, fn, first_share, start_bit, window, text_len, block, threads):
+            import vafc
+            calls["gz_shares"] += 1
+            try:
+                st, ri, crc, reads = vafc.scan_gz_share(fn, self.k, first_share, start_bit, window, text_len, block,
+                                                        threads, with_reads=True)
+            except FileNotFoundError:
+                return False, 0, 0, (D.NO_OFFSET, D.NO_OFFSET, 0, 0), None
+            if reads:
+                lens = np.array([len(r) for r in reads], np.uint32)
+                offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+                seq = np.frombuffer(b"".join(reads), np.uint8)
+                c, km = self.orc.count_reads(seq, offs, lens, self.n)
+                self.counts[:2 * self.n] += c
+                self.km += km
+            return True, st.bases, st.seqs, (ri.first, ri.next, ri.errs, ri.stopped), crc
 
         def save(self):
             self._saved = (self.counts.copy(), self.km)
@@ -238,7 +258,9 @@ def _run_driver(entry, synth_dir, tmp_path, counter, world=2):
 
 @pytest.mark.parametrize("counter", ["oracle", pytest.param("hip", marks=pytest.mark.gpu)])
 @pytest.mark.parametrize("name,world", [(n, 2) for n in DIST_CASES] + [("c1_plumbing_k21", 3), ("pe_k31", 3),
-                                                                       ("mal_bg", 3)])
+                                                                       ("mal_bg", 3), ("c1_plumbing_k21_gz", 3),
+                                                                       ("gz_multi_k21", 3), ("gz_multi_k21", 5),
+                                                                       ("edge_gz", 3), ("gz_mixed_k21", 3)])
 def test_dist_driver_matches_reference(name, world, counter, manifest, synth_dir, tmp_path):
     """vafc_dist.run over gloo ranks (the oracle as the per-rank counter on
     CPU; the HIP counter, every rank on device 0, in the GPU suite): plain
@@ -272,6 +294,9 @@ def test_dist_driver_matches_reference(name, world, counter, manifest, synth_dir
     if counter == "oracle":
         if name in DIST_CLEAN:
             assert all(c["restores"] == 0 and c["ranges"] >= 1 for c in calls), calls
+        if name in DIST_GZ_CLEAN:   # every gzip file split into shares: nothing counted whole, nothing redone
+            assert all(c["restores"] == 0 and c["whole"] == 0 for c in calls), calls
+            assert sum(c["gz_shares"] for c in calls) >= (world if name != "edge_gz" else 1), calls
         if name.startswith("mal_") or name == "truncated":
             assert all(c["restores"] >= 1 for c in calls), calls
 
@@ -286,3 +311,20 @@ def test_dist_driver_usage_and_missing_patterns(tmp_path):
     assert D.run(["-p", str(tmp_path / "none.txt"), "-o", str(tmp_path / "o.vaf"), "x.fq"], None,
                  err=lines.append) == 1
     assert "failed to load pattern file" in "".join(lines)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_driver_gzip_bad_crc_falls_back(world, manifest, synth_dir, tmp_path):
+    """A gzip file whose middle member fails its CRC-32 check: the shares are
+    counted, the combined check fails, and the file is counted whole by one
+    rank -- the same .vaf as the single-rank driver (gzread's output around a
+    failed check is buffer-dependent, so there is no reference golden)."""
+    entry = {"name": "gz_badcrc", "argv": ["-v", "-k", "21", "-t", "2", "-p", "grch38_k21.txt", "c1_10k_badcrc.fq.gz"],
+             "inputs": ["synth:grch38_k21.txt", "synth:c1_10k_badcrc.fq.gz"]}
+    (tmp_path / "w1").mkdir()
+    rcs1, stats1, data1, _, _ = _run_driver(entry, synth_dir, tmp_path / "w1", "oracle", 1)
+    rcs, stats, data, err, calls = _run_driver(entry, synth_dir, tmp_path, "oracle", world)
+    assert rcs == [0] * world and rcs1 == [0], err[-2000:]
+    assert data == data1 and stats == stats1
+    assert all(c["restores"] >= 1 for c in calls), calls
+    assert sum(c["whole"] for c in calls) == 1 and sum(c["gz_shares"] for c in calls) >= 2, calls

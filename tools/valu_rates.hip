@@ -1,14 +1,18 @@
 // valu_rates.hip -- issue cost of the VALU instructions the counting kernel
 // uses, measured on the device (tools only, never shipped).  Every wave runs
 // 8 independent chains of one instruction (inline asm, so the compiler keeps
-// exactly that instruction), 16 waves per CU (4 per SIMD) on every CU; the
-// time per instruction per SIMD is kernel time / (4 waves * instructions per
-// wave).
-//   hipcc --offload-arch=gfx950 -O3 -o tools/valu_rates tools/valu_rates.hip && tools/valu_rates
+// exactly that instruction), W waves per SIMD on every CU (W = 1, 2, 4, 8:
+// blocks of 256 / 512 / 1024 threads, one per CU, or two 1024-thread blocks
+// per CU); the time per instruction per SIMD is kernel time / (W waves *
+// instructions per wave).  Round 6 added the occupancy sweep: is the 2.7-3.0
+// cycles measured at 4 waves per SIMD an occupancy artefact (the guide gives
+// 2 cycles per wave64 VALU instruction on a 32-wide SIMD)?
+//   hipcc --offload-arch=gfx950 -O3 -o tools/valu_rates tools/valu_rates.hip && tools/valu_rates [W ...]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 
-#define ITERS 4096
+#define ITERS 16384
 
 #define CHAIN8(INS)                                                                                    \
 	asm volatile(INS : "+v"(a0) : "v"(s0), "v"(s1));                                                  \
@@ -55,15 +59,14 @@ KERNEL(k_cndmask_vcc, "v_cndmask_b32 %0, %0, %1, vcc")
 
 typedef void (*kfn)(unsigned *, unsigned);
 
-int main()
+int main(int argc, char **argv)
 {
 	int cus = 0;
 	hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
 	int clk_khz = 0;
 	hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, 0);
 	unsigned *out;
-	const int blocks = cus;     // one 1024-thread block (16 waves = 4 per SIMD) per CU
-	hipMalloc(&out, (size_t)blocks * 1024 * 4);
+	hipMalloc(&out, (size_t)2 * cus * 1024 * 4);
 	struct { const char *name; kfn f; } ks[] = {
 		{"v_add_u32", k_add_u32}, {"v_and_b32", k_and_b32}, {"v_lshrrev_b32", k_lshrrev_b32},
 		{"v_lshl_or_b32", k_lshl_or_b32}, {"v_alignbit_b32", k_alignbit_b32}, {"v_alignbyte_b32", k_alignbyte_b32},
@@ -76,23 +79,39 @@ int main()
 	hipEvent_t e0, e1;
 	hipEventCreate(&e0);
 	hipEventCreate(&e1);
-	printf("CUs %d, reported clock %.0f MHz, %d instructions per wave per kernel\n", cus, clk_khz / 1e3, ITERS * 8);
-	for (auto &k : ks) {
-		float best = 1e30f;
-		for (int rep = 0; rep < 5; ++rep) {
-			hipEventRecord(e0, 0);
-			hipLaunchKernelGGL(k.f, dim3(blocks), dim3(1024), 0, 0, out, (unsigned)rep);
-			hipEventRecord(e1, 0);
-			hipEventSynchronize(e1);
-			float ms;
-			hipEventElapsedTime(&ms, e0, e1);
-			if (rep && ms < best) best = ms;
-		}
-		const double instr_per_simd = 4.0 * ITERS * 8;     // 4 waves per SIMD
-		const double ns_per_instr = best * 1e6 / instr_per_simd;
-		printf("%-18s %8.3f ms  %.3f ns per wave-instruction per SIMD  (%.2f cycles at 2.4 GHz)\n", k.name, best,
-		       ns_per_instr, ns_per_instr * 2.4);
+	int ws[8] = {1, 2, 4, 8}, nw = 4;
+	if (argc > 1) {
+		nw = 0;
+		for (int i = 1; i < argc && nw < 8; ++i) ws[nw++] = atoi(argv[i]);
 	}
+	printf("CUs %d, reported clock %.0f MHz, %d instructions per wave per kernel\n", cus, clk_khz / 1e3, ITERS * 8);
+	printf("%-18s", "cycles/instr/SIMD");
+	for (int w = 0; w < nw; ++w) printf("  W=%d waves/SIMD", ws[w]);
+	printf("\n");
+	for (auto &k : ks) {
+		printf("%-18s", k.name);
+		for (int w = 0; w < nw; ++w) {
+			const int W = ws[w];
+			// W waves per SIMD = 4 W per CU: one block of 256 W threads per CU up
+			// to 1024, else 4W/16 blocks of 1024 per CU
+			const int threads = W <= 4 ? 256 * W : 1024, blocks = W <= 4 ? cus : cus * (W / 4);
+			float best = 1e30f;
+			for (int rep = 0; rep < 5; ++rep) {
+				hipEventRecord(e0, 0);
+				hipLaunchKernelGGL(k.f, dim3(blocks), dim3(threads), 0, 0, out, (unsigned)rep);
+				hipEventRecord(e1, 0);
+				hipEventSynchronize(e1);
+				float ms;
+				hipEventElapsedTime(&ms, e0, e1);
+				if (rep && ms < best) best = ms;
+			}
+			const double instr_per_simd = (double)W * ITERS * 8;
+			const double ns_per_instr = best * 1e6 / instr_per_simd;
+			printf("  %7.2f (%6.3f ms)", ns_per_instr * 2.4, best);
+		}
+		printf("\n");
+	}
+	printf("(cycles at 2.4 GHz per wave-instruction per SIMD; kernel time in parentheses)\n");
 	hipFree(out);
 	return 0;
 }
