@@ -295,3 +295,90 @@ def test_parallel_parse_of_gzip_stops_early_without_reading_on(tmp_path, monkeyp
         st1, r1 = vafc.scan_file_parallel(p, 21, 1, threads=4, piece_bytes=4096, with_reads=True)
         assert (st1.bases, st1.seqs, st1.blocks) == (st0.bases, st0.seqs, st0.blocks)
         assert r1 == r0 and st0.seqs == 30
+
+
+# --------------------------------------------------------------------------
+# shares of one gzip stream over several ranks (round 6; include/vafc.h
+# vc_gz_share_scan / vc_scan_gz_share, kmer-cnt_amd/vafc_dist.py), driven here
+# in one process: every share's reads in order == the sequential reader's
+# --------------------------------------------------------------------------
+
+def _shares(path, world, k=5, block=100, chunk=16 << 10, threads=3):
+    """Scan, chain and count the `world` shares of a gzip file; returns
+    (chained, ranges, crcs, reads in share order)."""
+    import vafc
+    import vafc_dist as D
+    size = os.path.getsize(path)
+    rows, wsyms = [], []
+    for r in range(world):
+        b, e = D.byte_range(size, r, world)
+        if e <= b:
+            rows.append((D.NO_OFFSET, D.NO_OFFSET, 0, 1, 0))
+            wsyms.append(np.zeros(vafc.GZ_WSIZE, np.uint16))
+            continue
+        info, w = vafc.gz_share_scan(path, b, e, threads=threads, chunk_bytes=chunk)
+        rows.append((info["start_bit"], info["end_bit"], info["text_len"], info["ok"], info["ended"]))
+        wsyms.append(w)
+    if not D.gz_shares_chain(rows):
+        return False, None, None, None
+    wins = D.gz_windows(rows, wsyms)
+    ranges, crcs, reads = [], [], []
+    for r in range(world):
+        if rows[r][0] == D.NO_OFFSET:
+            ranges.append((D.EMPTY_RANGE, D.EMPTY_RANGE, 0, 0))
+            continue
+        st, ri, cr, rd = vafc.scan_gz_share(path, k, r == 0, rows[r][0], wins[r], rows[r][2], block, threads,
+                                            with_reads=True)
+        ranges.append((ri.first, ri.next, ri.errs, ri.stopped))
+        crcs.append(cr)
+        reads += rd
+    return True, ranges, crcs, reads
+
+
+@pytest.mark.parametrize("shape", ["one", "pigz", "multi", "fixed_blocks"])
+@pytest.mark.parametrize("world", [2, 3, 7])
+def test_gzip_shares_reproduce_the_stream(tmp_path, text, shape, world):
+    """Every share decoded blind, chained by its window, and counted from its
+    start: the shares' reads in order are the sequential reader's, the
+    ranges chain, and the members' CRC-32 checks combine across the shares."""
+    import vafc
+    import vafc_dist as D
+    p = str(tmp_path / "s.fq.gz")
+    if shape == "one":
+        data = _member(text, level=1)
+    elif shape == "pigz":      # sync-flushed pieces: empty stored blocks between them
+        c = zlib.compressobj(1, zlib.DEFLATED, -15)
+        body = b"".join(c.compress(text[a:a + 60000]) + c.flush(zlib.Z_SYNC_FLUSH)
+                        for a in range(0, len(text), 60000)) + c.flush()
+        data = b"\x1f\x8b\x08\x00\x00\x00\x00\x00\x04\x03" + body + struct.pack("<II", zlib.crc32(text), len(text))
+    elif shape == "multi":     # members cut inside records
+        cut = [0, len(text) // 3 + 11, 2 * len(text) // 3 + 5, len(text)]
+        data = b"".join(_member(text[a:b], level=1) for a, b in zip(cut, cut[1:]))
+    else:                      # fixed-Huffman blocks only: no later share can start blind,
+        data = _member(text, level=1, strategy=zlib.Z_FIXED)   # so share 0 decodes to the end
+    with open(p, "wb") as f:
+        f.write(data)
+    chained, ranges, crcs, reads = _shares(p, world)
+    assert chained
+    if shape == "fixed_blocks":
+        assert all(r[0] == D.EMPTY_RANGE for r in ranges[1:])
+    st0, r0 = vafc.scan_file(p, 5, 100, with_reads=True)
+    assert reads == r0
+    assert D.chain_holds(ranges)
+    assert D.gz_crc_chain(crcs, vafc.gz_crc32_combine)
+
+
+def test_gzip_shares_bad_crc_is_caught(tmp_path, text):
+    """A wrong CRC-32 in a member that spans two shares: each share alone
+    cannot see it; the combined check does."""
+    import vafc
+    import vafc_dist as D
+    p = str(tmp_path / "bad.fq.gz")
+    m = bytearray(_member(text, level=1))
+    m[-8] ^= 0x01
+    with open(p, "wb") as f:
+        f.write(bytes(m))
+    chained, ranges, crcs, reads = _shares(p, 3)
+    assert chained and D.chain_holds(ranges)
+    assert not D.gz_crc_chain(crcs, vafc.gz_crc32_combine)
+    assert all(c["crc_error"] == 0 for c in crcs)

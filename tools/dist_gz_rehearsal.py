@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""One gzip FASTQ over torchrun-style ranks on one GPU box (tools only): the
+split-gzip path of kmer-cnt_amd/vafc_dist.py (shares of the deflate stream,
+vafc_gzip.h) against the same driver at one rank.  Writes --reads reads of the
+C2 stream as FASTQ in /dev/shm, gzips it the pigz way at level 1
+(bench.gzip_level1), then runs the driver at 1 rank (-t T) and at N ranks
+(-t T/N each, gloo, VAFC_REHEARSAL=1: every rank on GPU 0, so the N ranks
+share the one box's CPU share), alternately, and prints one JSON object: each
+run's counting Speed line (the reference's metric), per-file line and .vaf md5.
+
+    python tools/dist_gz_rehearsal.py [--reads 30000000] [--ranks 2] [--rounds 2]
+"""
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "kmer-cnt_amd"))
+DRIVER = os.path.join(ROOT, "kmer-cnt_amd", "vafc_dist.py")
+
+
+def run(n, threads, pat, gz, out, timeout=600):
+    env = dict(os.environ, VAFC_DIST_BACKEND="gloo", VAFC_REHEARSAL="1")
+    argv = ["-v", "-k", "21", "-t", str(threads), "-p", pat, "-o", out, gz]
+    t0 = time.time()
+    if n == 1:
+        env.pop("WORLD_SIZE", None)
+        p = subprocess.run([sys.executable, DRIVER] + argv, env=env, capture_output=True, text=True, timeout=timeout)
+        err, rc = p.stderr, p.returncode
+    else:
+        import bench
+        logf = out + ".err"
+        with open(logf, "w") as f:
+            port = bench.free_port()
+            procs = []
+            for r in range(n):
+                e = dict(env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                         MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                procs.append(subprocess.Popen([sys.executable, DRIVER] + argv, env=e, stdout=subprocess.DEVNULL,
+                                              stderr=f if r == 0 else subprocess.DEVNULL))
+            rc = 0
+            for p in procs:
+                rc = rc or p.wait(timeout=timeout)
+        err = open(logf).read()
+    wall = time.time() - t0
+    m = re.search(r"Speed:\s+([0-9.]+) Mbases/sec", err)
+    per_file = re.findall(r"^\[V::count_fastq_kmers\].*$", err, re.M)
+    if rc != 0 or not m:
+        raise RuntimeError("driver at %d rank(s) failed (%d): %s" % (n, rc, err[-2000:]))
+    return {"mbases": float(m.group(1)), "process_wall_s": round(wall, 2), "per_file": per_file,
+            "counting": re.search(r"K-mer counting:\s+([0-9.]+) sec", err).group(1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=30_000_000)
+    ap.add_argument("--ranks", type=int, default=2)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--threads", type=int, default=16, help="reader threads of the box (split over the ranks)")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import bench
+    import vafc
+    import vafc_synth as S
+    dev = torch.device("cuda", 0)
+    panel = S.grch38_panel()
+    tmp = tempfile.mkdtemp(prefix="vafc_gzr_")
+    pat = os.path.join(tmp, "p.txt")
+    panel.write_patterns(pat, 21)
+    R, L = a.reads, 150
+    d_seq = torch.empty(R * L, dtype=torch.uint8, device=dev)
+    d_offs = torch.empty(R, dtype=torch.int64, device=dev)
+    d_lens = torch.empty(R, dtype=torch.int32, device=dev)
+    win = torch.from_numpy(panel.windows().reshape(-1)).to(dev)
+    dos = torch.from_numpy(panel.dosage.astype(np.uint8)).to(dev)
+    vafc.synth_reads(d_seq.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), 0, R, L, S.READ_SEED_R1, 0.01,
+                     win.data_ptr(), dos.data_ptr(), panel.n, 0)
+    torch.cuda.synchronize()
+    work = bench.scratch_dir(R * (2 * L + 16) * 1.5, tmp)
+    fq = os.path.join(work, "c2.fq")
+    bench.write_fastq_from_device(d_seq, R, L, fq, threads=a.threads)
+    del d_seq, d_offs, d_lens
+    torch.cuda.empty_cache()
+    gz = fq + ".gz"
+    gz_bytes = bench.gzip_level1(fq, gz, a.threads)
+    text = os.path.getsize(fq)
+    os.unlink(fq)
+    sys.stderr.write("[gzr] %d reads, %.2f GB of text, %.2f GB gzip\n" % (R, text / 1e9, gz_bytes / 1e9))
+    out = {"workload": "%dM x %d bp reads of the C2 stream as one pigz-shaped level-1 gzip FASTQ (%.2f GB, %.2f GB "
+                       "of text) in the page cache; k = 21, the GRCh38 panel" % (R // 10**6, L, gz_bytes / 1e9,
+                                                                                text / 1e9),
+           "box": "one GPU box, %d reader threads in all: 1 rank x %d against %d ranks x %d (gloo, every rank on "
+                  "GPU 0)" % (a.threads, a.threads, a.ranks, max(1, a.threads // a.ranks)),
+           "runs": {"1": [], str(a.ranks): []}}
+    md5s = {}
+    run(1, a.threads, pat, gz, os.path.join(tmp, "warm.vaf"))
+    for rep in range(a.rounds):
+        for n in (1, a.ranks):
+            o = os.path.join(tmp, "r%d.vaf" % n)
+            r = run(n, max(1, a.threads // n), pat, gz, o)
+            md5s[n] = bench.md5(o)
+            out["runs"][str(n)].append(r)
+            sys.stderr.write("[gzr] %d rank(s), round %d: %.1f Mbases/s\n" % (n, rep + 1, r["mbases"]))
+    out["vaf_identical"] = md5s[1] == md5s[a.ranks]
+    out["note"] = ("the split-gzip pass decodes each share twice (a blind scan for the window chain, then the "
+                   "counting pass), so at a fixed CPU share N ranks do about twice the single rank's inflate "
+                   "work; with a CPU share per rank (one per GPU) the pass takes about 2/N of the single rank's")
+    print(json.dumps(out))
+    os.unlink(gz)
+    if work != tmp:
+        shutil.rmtree(work, ignore_errors=True)
+    shutil.rmtree(tmp, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
