@@ -349,6 +349,17 @@ struct Out {
 		free(t);
 	}
 	size_t total() const { return wide ? ns : nt; }
+	// bytes written (the buffers' caps are address space, faulted in as
+	// written), with a huge page of slack for each
+	size_t held() const { return ns * sizeof(uint16_t) + nt + ((size_t)4 << 20); }
+	void release_buffers()
+	{
+		free(s);
+		free(t);
+		s = nullptr;
+		t = nullptr;
+		ns = nt = caps = capt = res = 0;
+	}
 	void reset(bool known_history)
 	{
 		ns = nt = res = 0;
@@ -360,7 +371,11 @@ struct Out {
 	static bool grow_buf(void **p, size_t *cap, size_t need, size_t elem)
 	{
 		if (need > OUT_CAP + 4096) return false;
-		size_t nc = *cap ? *cap : ((size_t)1 << 20);
+		// the whole cap at once: beyond the mmap threshold, so the pages are
+		// faulted in as written and nothing is ever copied by a regrow (a
+		// chain of reallocs from 1 MiB cost as much as the decode for chunks
+		// in fresh buffers, as a held share's are)
+		size_t nc = *cap ? *cap : OUT_CAP + 4096;
 		while (nc < need) nc *= 2;
 		void *q = realloc(*p, nc * elem);
 		if (!q) return false;
@@ -710,7 +725,7 @@ struct Chunk {
 	bool decoded = false;
 	bool known = false;               // starts at the stream's first block (empty history, no search)
 	bool end_dynamic = false;         // share scans: stop only at a dynamic block (one a search can find)
-	std::unique_ptr<Tables> tab{new Tables};
+	std::unique_ptr<Tables> tab;      // allocated by the first decode (a held share keeps many chunks)
 };
 
 // After a final block: the member trailer, then the next member's header.
@@ -835,6 +850,7 @@ bool plausible_next(const uint8_t *p, uint64_t n, uint64_t b, Tables &scratch)
 
 void decode_chunk(const uint8_t *p, uint64_t n, uint64_t first_bit, Chunk &C)
 {
+	if (!C.tab) C.tab.reset(new Tables);
 	C.ok = C.stream_end = false;
 	C.start = -1;
 	C.events.clear();
@@ -1073,6 +1089,7 @@ struct GzShareOpts {
 	uint64_t start_bit = 0;           // stream, later shares: the share's first block
 	const uint8_t *window = nullptr;  // stream, later shares: the 32 KiB before it
 	uint64_t text_len = UINT64_MAX;   // stream: the share's text (CRC accounting)
+	uint64_t hold_bytes = 0;          // scan: keep the decoded share (at most this many bytes) for resume()
 };
 
 class VcGzParallel {
@@ -1092,6 +1109,12 @@ public:
 		std::lock_guard<std::mutex> lk(mu_);
 		*out = scrc_;
 	}
+	// scan mode: the scan kept every chunk of the share (vc_gzp_scan_share_hold)
+	bool held() const { return held_; }
+	// A held share: stream its text from the kept chunks with the now known
+	// window before it (nullptr: the stream's first share), then on past its
+	// end with zlib, in small pieces, as far as the reader asks.
+	bool resume(const uint8_t *window, uint64_t text_len);
 	int64_t read(uint8_t *dst, size_t n);
 	int64_t span(const uint8_t **out, size_t maxn, void **hold = nullptr);
 	void release(void *hold);
@@ -1139,6 +1162,11 @@ private:
 	uint64_t pbase_ = 0;              // text offset of cur_'s first byte
 	bool crc_stopped_ = false;
 	VcGzShareCrc scrc_;
+	bool hold_ = false, held_ = false;   // scan: keeping the share's chunks / kept all of them
+	uint64_t hold_budget_ = 0, held_bytes_ = 0;
+	bool continue_after_ = false;     // resumed share: zlib on past the last kept chunk
+	uint64_t scan_pos_ = UINT64_MAX / 2;   // held scan: the chunk the scan waits for (bounds decode-ahead)
+	int threads_ = 1;
 
 	void worker();
 	void sequencer();
@@ -1153,7 +1181,7 @@ private:
 		scrc_.complete = stats.crc_error ? 0u : 1u;
 		crc_stopped_ = true;
 	}
-	bool fallback(uint64_t &expect, uint64_t nom_b, bool &ended);
+	bool fallback(uint64_t &expect, uint64_t nom_b, bool &ended, size_t piece_cap = PIECE_CAP);
 	Piece *new_piece();
 	bool push_piece(std::unique_ptr<Piece> P);   // waits for queue space; false on stop
 	void window_append(const uint8_t *t, size_t n);
@@ -1213,7 +1241,9 @@ void VcGzParallel::worker()
 					task = P.get();
 					return true;
 				}
-			if (next_decode_ < nchunks_) {
+			// a held share has a slot per chunk: decode at most a slot ring's
+			// worth ahead of the scan, as the ring itself bounds ordinary runs
+			if (next_decode_ < nchunks_ && next_decode_ < scan_pos_ + (uint64_t)threads_ + 2) {
 				Chunk &C = *slots_[next_decode_ % slots_.size()];
 				if (!C.busy) {
 					dec = &C;
@@ -1268,7 +1298,7 @@ void VcGzParallel::worker()
 // zlib from the true boundary `expect` with the true history, until the first
 // block start at or past nom_b, the end of the stream, or an error.  Output
 // goes to pieces of at most PIECE_CAP bytes.  false only on stop / no memory.
-bool VcGzParallel::fallback(uint64_t &expect, uint64_t nom_b, bool &ended)
+bool VcGzParallel::fallback(uint64_t &expect, uint64_t nom_b, bool &ended, size_t piece_cap)
 {
 	z_stream zs;
 	memset(&zs, 0, sizeof zs);
@@ -1294,21 +1324,21 @@ bool VcGzParallel::fallback(uint64_t &expect, uint64_t nom_b, bool &ended)
 		P->ready = true;
 		return push_piece(std::move(P));
 	};
-	bool alive = P->reserve(PIECE_CAP);
+	bool alive = P->reserve(piece_cap);
 	while (alive) {
-		if (P->n == P->cap) {   // piece full
+		if (P->n >= piece_cap) {   // piece full
 			if (!emit(false)) {
 				alive = false;
 				break;
 			}
 			P.reset(new_piece());
-			if (!P->reserve(PIECE_CAP)) {
+			if (!P->reserve(piece_cap)) {
 				alive = false;
 				break;
 			}
 		}
 		zs.next_out = P->text + P->n;
-		zs.avail_out = (uInt)(P->cap - P->n);
+		zs.avail_out = (uInt)(piece_cap - P->n);
 		const int ret = inflate(&zs, Z_BLOCK);
 		const size_t made = (size_t)(zs.next_out - (P->text + P->n));
 		window_append(P->text + P->n, made);
@@ -1435,6 +1465,10 @@ void VcGzParallel::sequencer()
 		}
 		if (!fallback(expect, C->nom_b, ended)) break;
 	}
+	// a resumed share: its last record may end in the next share, which no
+	// chunk covers -- zlib on from the share's end in small pieces (the reader
+	// stops after a few KiB, and the pass waits for each piece)
+	if (continue_after_ && !ended && !stop_) fallback(expect, UINT64_MAX, ended, (size_t)256 << 10);
 	std::lock_guard<std::mutex> lk(mu_);
 	seq_done_ = true;
 	cv_.notify_all();
@@ -1457,13 +1491,20 @@ void VcGzParallel::scan_sequencer()
 		Chunk *C = slots_[j % slots_.size()].get();
 		{
 			std::unique_lock<std::mutex> lk(mu_);
+			if (slots_.size() >= nchunks_) {   // a slot per chunk (held, or over the budget since)
+				scan_pos_ = j;
+				cv_.notify_all();
+			}
 			cv_.wait(lk, [&] { return stop_ || (C->index == j && C->decoded); });
 			if (stop_) {
 				ok = false;
 				break;
 			}
 		}
+		// one slot per chunk (a held share): a chunk's buffers are freed with it
+		const bool per_chunk = slots_.size() >= nchunks_;
 		auto release = [&]() {
+			if (per_chunk) C->out.release_buffers();
 			std::lock_guard<std::mutex> lk(mu_);
 			C->busy = false;
 			cv_.notify_all();
@@ -1504,14 +1545,62 @@ void VcGzParallel::scan_sequencer()
 		member_text_ = C->events.empty() ? member_text_ + n : n - C->events.back().off;
 		expect = C->end;
 		ended = C->stream_end;
+		if (hold_ && held_bytes_ + o.held() <= hold_budget_) {   // kept for resume(): stays busy
+			held_bytes_ += o.held();
+			continue;
+		}
+		if (hold_) {   // over the budget: the share will be decoded again; free what was kept
+			hold_ = false;
+			std::lock_guard<std::mutex> lk(mu_);
+			for (uint64_t i = 0; i < j; ++i) {
+				Chunk *K = slots_[i % slots_.size()].get();
+				if (K->busy && K->index == i && K->decoded) {
+					K->out.release_buffers();
+					K->busy = false;
+				}
+			}
+			cv_.notify_all();
+		}
 		release();
 	}
 	std::lock_guard<std::mutex> lk(mu_);
+	held_ = hold_ && ok && share_.start_bit != UINT64_MAX;
 	share_.ok = ok;
 	share_.text_len = share_.start_bit == UINT64_MAX ? 0 : len;
 	share_.end_bit = ended || share_.start_bit == UINT64_MAX ? UINT64_MAX : expect;
 	seq_done_ = true;
 	cv_.notify_all();
+}
+
+bool VcGzParallel::resume(const uint8_t *window, uint64_t text_len)
+{
+	{
+		std::unique_lock<std::mutex> lk(mu_);
+		cv_.wait(lk, [&] { return seq_done_; });
+		if (!held_) return false;
+	}
+	if (seq_.joinable()) seq_.join();
+	scan_ = false;
+	share_len_ = text_len;
+	continue_after_ = true;
+	if (window) {   // a later share: its history is the window before it
+		memcpy(window_.data(), window, WSIZE);
+		member_text_ = WSIZE;
+	} else {
+		member_text_ = 0;
+	}
+	first_bit_ = share_.start_bit;
+	max_pieces_ = (size_t)threads_ + 4;
+	{
+		std::lock_guard<std::mutex> lk(mu_);
+		seq_done_ = false;
+	}
+	const VcCpuSet cpus = vc_affinity_get();
+	seq_ = std::thread([this, cpus] {
+		vc_affinity_bind(cpus);
+		sequencer();
+	});
+	return true;
 }
 
 // The reader has delivered the share's last byte, at offset `cut` of piece P
@@ -1545,6 +1634,9 @@ bool VcGzParallel::start(const char *path, int threads, uint64_t chunk_bytes, co
 	last_bit_ = n_ * 8;
 	if (so && so->scan) {
 		scan_ = true;
+		hold_ = so->hold_bytes > 0;
+		hold_budget_ = so->hold_bytes;
+		if (hold_) scan_pos_ = 0;
 		if (so->begin > 0) {   // a later share: its first block is searched for
 			known_start_ = false;
 			first_bit_ = std::max<uint64_t>(first_bit_, std::min<uint64_t>(so->begin, n_) * 8);
@@ -1578,7 +1670,10 @@ bool VcGzParallel::start(const char *path, int threads, uint64_t chunk_bytes, co
 	if (threads < 1) threads = 1;
 	size_t extra = 2;
 	if (const char *e = getenv("VAFC_GZ_SLOTS")) extra = (size_t)atoi(e);   // A/B knob: slots beyond the workers
-	slots_.resize((size_t)threads + extra);
+	// a held share keeps every chunk (hold_budget_ bounds their buffers; a
+	// chunk's decode tables are allocated by its first decode)
+	slots_.resize(hold_ ? (size_t)nchunks_ + extra : (size_t)threads + extra);
+	threads_ = threads;
 	for (auto &s : slots_) s.reset(new Chunk);
 	max_pieces_ = (size_t)threads + extra + 2;
 	fixed_tables();
@@ -1800,6 +1895,31 @@ bool vc_gzp_scan_share(const char *path, int threads, uint64_t chunk_bytes, uint
 	return true;
 }
 
+bool vc_gzp_scan_share_hold(const char *path, int threads, uint64_t chunk_bytes, uint64_t begin, uint64_t end,
+                            uint64_t hold_bytes, VcGzShare *sh, uint16_t *window_sym, VcGzParallel **held)
+{
+	GzShareOpts so;
+	so.scan = true;
+	so.begin = begin;
+	so.end = end;
+	so.hold_bytes = hold_bytes;
+	*held = nullptr;
+	VcGzParallel *g = new VcGzParallel;
+	if (!g->start(path, threads, chunk_bytes, &so)) {
+		delete g;
+		return false;
+	}
+	g->scan_result(sh, window_sym);
+	if (g->held()) *held = g;
+	else delete g;
+	return true;
+}
+
+bool vc_gzp_resume_share(VcGzParallel *g, const uint8_t *window, uint64_t text_len)
+{
+	return g->resume(window, text_len);
+}
+
 VcGzParallel *vc_gzp_open_share(const char *path, int threads, uint64_t chunk_bytes, bool first_share,
                                 uint64_t start_bit, const uint8_t *window, uint64_t text_len)
 {
@@ -1870,6 +1990,39 @@ extern "C" uint32_t vc_gz_crc32(uint32_t crc, const uint8_t *p, uint64_t n) { re
 extern "C" uint32_t vc_gz_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2)
 {
 	return (uint32_t)crc32_combine64(crc1, crc2, (z_off64_t)len2);
+}
+
+int vc_gz_text_format(const char *path);   // vafc_ingest.cpp
+
+extern "C" int vc_gz_share_open(const char *path, uint64_t begin, uint64_t end, int n_threads, uint64_t chunk_bytes,
+                                uint64_t hold_bytes, vc_gz_share_info *out, uint16_t *window_sym, vc_gz_share **held)
+{
+	if (!path || !out || !held || end <= begin) return VC_EINVAL;
+	*held = nullptr;
+	const int t = n_threads < 1 ? 1 : n_threads;
+	VcGzShare sh;
+	VcGzParallel *g = nullptr;
+	if (!vc_gzp_scan_share_hold(path, t, chunk_bytes, begin, end, hold_bytes, &sh, window_sym, &g)) return VC_EIO;
+	out->start_bit = sh.start_bit;
+	out->end_bit = sh.end_bit;
+	out->text_len = sh.text_len;
+	out->ok = sh.ok ? 1u : 0u;
+	out->ended = sh.start_bit != UINT64_MAX && sh.end_bit == UINT64_MAX ? 1u : 0u;
+	if (g) {
+		vc_gz_share *h = new vc_gz_share;
+		h->g = g;
+		h->format = vc_gz_text_format(path);
+		h->threads = t;
+		*held = h;
+	}
+	return VC_OK;
+}
+
+extern "C" void vc_gz_share_close(vc_gz_share *h)
+{
+	if (!h) return;
+	if (h->g) vc_gzp_close(h->g);
+	delete h;
 }
 
 extern "C" int vc_gz_share_scan(const char *path, uint64_t begin, uint64_t end, int n_threads, uint64_t chunk_bytes,

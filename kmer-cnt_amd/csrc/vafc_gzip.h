@@ -105,6 +105,23 @@ struct VcGzShareCrc {
 VcGzParallel *vc_gzp_open_share(const char *path, int threads, uint64_t chunk_bytes, bool first_share,
                                 uint64_t start_bit, const uint8_t *window, uint64_t text_len);
 void vc_gzp_share_crc(VcGzParallel *g, VcGzShareCrc *out);
+// The scan of vc_gzp_scan_share keeping the share's decoded chunks (about 3
+// bytes per byte of text, at most hold_bytes of buffers), so that the count
+// resumes from them instead of inflating the share again: *held is the open
+// inflater (close with vc_gzp_close), or nullptr when the share did not fit
+// (or could not be scanned).  false if the file cannot be opened as gzip.
+bool vc_gzp_scan_share_hold(const char *path, int threads, uint64_t chunk_bytes, uint64_t begin, uint64_t end,
+                            uint64_t hold_bytes, VcGzShare *sh, uint16_t *window_sym, VcGzParallel **held);
+// Stream a held share (as vc_gzp_open_share would from its start) with the
+// window before it (nullptr: the stream's first share).
+bool vc_gzp_resume_share(VcGzParallel *g, const uint8_t *window, uint64_t text_len);
+
+// The C ABI's handle of a held share (include/vafc.h vc_gz_share_open).
+struct vc_gz_share {
+	VcGzParallel *g = nullptr;
+	int format = -1;    // FASTA 1 / FASTQ 0 by the stream's first header (vc_gz_text_format)
+	int threads = 1;
+};
 // Next bytes of the decompressed stream, in order: > 0 bytes, 0 at the end.
 int64_t vc_gzp_read(VcGzParallel *g, uint8_t *dst, size_t n);
 // The same without a copy: up to `max` next bytes at *p, valid until the next

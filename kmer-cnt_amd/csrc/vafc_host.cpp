@@ -1617,27 +1617,14 @@ extern "C" int vc_count_file_range(vc_ctx *c, const char *path, uint64_t begin, 
 	return rc;
 }
 
-// One share of a gzip file (include/vafc.h, vafc_gzip.h): the inflater from
-// the share's first block with its known window, the parallel reader over the
-// share's text as a range (plus the previous byte, for the first guess).
-extern "C" int vc_count_gz_share(vc_ctx *c, const char *path, int first_share, uint64_t start_bit,
-                                 const uint8_t *window, uint64_t text_len, int block_bases, int n_threads,
-                                 vc_file_stats *st, vc_range_info *ri, vc_gz_share_crc *crc)
+// One share of a gzip file (include/vafc.h, vafc_gzip.h): the inflater (from
+// the share's first block with its known window, or a held share resumed),
+// the parallel reader over the share's text as a range (plus the previous
+// byte, for the first guess).  Takes g and closes it.
+static int count_gz_share_g(vc_ctx *c, VcGzParallel *g, int fmt, int t, int first_share, const uint8_t *window,
+                            uint64_t text_len, int block_bases, vc_file_stats &local, vc_range_info *ri,
+                            vc_gz_share_crc *crc)
 {
-	if (!c || !path || !ri || !crc || text_len == 0 || (!first_share && !window)) return VC_EINVAL;
-	vc_file_stats local = {0, 0, 0, 0.0};
-	*ri = vc_range_info{UINT64_MAX, UINT64_MAX, 0, 0, 0};
-	memset(crc, 0, sizeof *crc);
-	const double t0 = wall_now();
-	HIPCK(hipSetDevice(c->dev));
-	const int fmt = vc_gz_text_format(path);
-	if (fmt < 0) return VC_EINVAL;
-	const int t = clamp_threads(n_threads);
-	VcAffinityScope placement(gpu_cpus(c, vc_gz_inflate_threads(t) + vc_gz_parse_threads(t) + 2));
-	const char *ce = getenv("VAFC_GZ_CHUNK");   // test knob: compressed bytes per chunk
-	VcGzParallel *g = vc_gzp_open_share(path, vc_gz_inflate_threads(t), ce ? (uint64_t)atoll(ce) : 0,
-	                                    first_share != 0, start_bit, window, text_len);
-	if (!g) return VC_EIO;
 	const int parsers = vc_gz_parse_threads(t);
 	int rc = reserve_ingest(c, parsers, false);
 	VcTextRange R;
@@ -1661,6 +1648,53 @@ extern "C" int vc_count_gz_share(vc_ctx *c, const char *path, int first_share, u
 	                    R.next == UINT64_MAX ? UINT64_MAX : R.next - np - text_len, R.errs, R.stopped ? 1u : 0u, 0u};
 	*crc = vc_gz_share_crc{sc.events, sc.head_crc, sc.head_len, sc.head_expect_crc, sc.head_expect_isize,
 	                       sc.tail_crc, sc.tail_len, sc.crc_error, sc.complete};
+	return rc;
+}
+
+extern "C" int vc_count_gz_share(vc_ctx *c, const char *path, int first_share, uint64_t start_bit,
+                                 const uint8_t *window, uint64_t text_len, int block_bases, int n_threads,
+                                 vc_file_stats *st, vc_range_info *ri, vc_gz_share_crc *crc)
+{
+	if (!c || !path || !ri || !crc || text_len == 0 || (!first_share && !window)) return VC_EINVAL;
+	vc_file_stats local = {0, 0, 0, 0.0};
+	*ri = vc_range_info{UINT64_MAX, UINT64_MAX, 0, 0, 0};
+	memset(crc, 0, sizeof *crc);
+	const double t0 = wall_now();
+	HIPCK(hipSetDevice(c->dev));
+	const int fmt = vc_gz_text_format(path);
+	if (fmt < 0) return VC_EINVAL;
+	const int t = clamp_threads(n_threads);
+	VcAffinityScope placement(gpu_cpus(c, vc_gz_inflate_threads(t) + vc_gz_parse_threads(t) + 2));
+	const char *ce = getenv("VAFC_GZ_CHUNK");   // test knob: compressed bytes per chunk
+	VcGzParallel *g = vc_gzp_open_share(path, vc_gz_inflate_threads(t), ce ? (uint64_t)atoll(ce) : 0,
+	                                    first_share != 0, start_bit, window, text_len);
+	if (!g) return VC_EIO;
+	const int rc = count_gz_share_g(c, g, fmt, t, first_share, window, text_len, block_bases, local, ri, crc);
+	local.seconds = wall_now() - t0;
+	if (st) *st = local;
+	return rc;
+}
+
+extern "C" int vc_count_gz_share_held(vc_ctx *c, vc_gz_share *h, int first_share, const uint8_t *window,
+                                      uint64_t text_len, int block_bases, int n_threads, vc_file_stats *st,
+                                      vc_range_info *ri, vc_gz_share_crc *crc)
+{
+	if (!c || !h || !h->g || !ri || !crc || text_len == 0 || (!first_share && !window)) return VC_EINVAL;
+	vc_file_stats local = {0, 0, 0, 0.0};
+	*ri = vc_range_info{UINT64_MAX, UINT64_MAX, 0, 0, 0};
+	memset(crc, 0, sizeof *crc);
+	const double t0 = wall_now();
+	HIPCK(hipSetDevice(c->dev));
+	if (h->format < 0) return VC_EINVAL;
+	const int t = clamp_threads(n_threads);
+	VcAffinityScope placement(gpu_cpus(c, vc_gz_inflate_threads(t) + vc_gz_parse_threads(t) + 2));
+	VcGzParallel *g = h->g;
+	h->g = nullptr;   // counted once; count_gz_share_g closes it
+	if (!vc_gzp_resume_share(g, first_share ? nullptr : window, text_len)) {
+		vc_gzp_close(g);
+		return VC_EINVAL;
+	}
+	const int rc = count_gz_share_g(c, g, h->format, t, first_share, window, text_len, block_bases, local, ri, crc);
 	local.seconds = wall_now() - t0;
 	if (st) *st = local;
 	return rc;

@@ -1052,22 +1052,12 @@ extern "C" int vc_scan_file_range(const char *path, int k, int block_bases, int 
 	return rc;
 }
 
-extern "C" int vc_scan_gz_share(const char *path, int k, int first_share, uint64_t start_bit, const uint8_t *window,
-                                uint64_t text_len, int block_bases, int n_threads, vc_file_stats *st,
-                                vc_range_info *ri, vc_gz_share_crc *crc, uint8_t *seq_out, size_t seq_cap,
-                                uint32_t *lens_out, size_t lens_cap)
+// The host-only count of one gzip share from an open inflater (closed here).
+static int scan_gz_share_g(VcGzParallel *g, int fmt, int k, int first_share, const uint8_t *window, uint64_t text_len,
+                           int block_bases, int n_threads, vc_file_stats &local, vc_range_info *ri,
+                           vc_gz_share_crc *crc, uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out,
+                           size_t lens_cap)
 {
-	if (!path || !st || !ri || !crc || n_threads < 1 || text_len == 0 || (!first_share && !window)) return VC_EINVAL;
-	vc_file_stats local = {0, 0, 0, 0.0};
-	*ri = vc_range_info{UINT64_MAX, UINT64_MAX, 0, 0, 0};
-	memset(crc, 0, sizeof *crc);
-	const double t0 = mono_now();
-	const int fmt = vc_gz_text_format(path);
-	if (fmt < 0) return VC_EINVAL;
-	const char *ce = getenv("VAFC_GZ_CHUNK");   // test knob: compressed bytes per chunk
-	VcGzParallel *g = vc_gzp_open_share(path, vc_gz_inflate_threads(n_threads), ce ? (uint64_t)atoll(ce) : 0,
-	                                    first_share != 0, start_bit, window, text_len);
-	if (!g) return VC_EIO;
 	const char *pe = getenv("VAFC_INGEST_PIECE");
 	const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : ((uint64_t)16 << 20);
 	const int parsers = vc_gz_parse_threads(n_threads);
@@ -1086,6 +1076,52 @@ extern "C" int vc_scan_gz_share(const char *path, int k, int first_share, uint64
 	                    R.next == UINT64_MAX ? UINT64_MAX : R.next - np - text_len, R.errs, R.stopped ? 1u : 0u, 0u};
 	*crc = vc_gz_share_crc{c.events, c.head_crc, c.head_len, c.head_expect_crc, c.head_expect_isize, c.tail_crc,
 	                       c.tail_len, c.crc_error, c.complete};
+	return rc;
+}
+
+extern "C" int vc_scan_gz_share(const char *path, int k, int first_share, uint64_t start_bit, const uint8_t *window,
+                                uint64_t text_len, int block_bases, int n_threads, vc_file_stats *st,
+                                vc_range_info *ri, vc_gz_share_crc *crc, uint8_t *seq_out, size_t seq_cap,
+                                uint32_t *lens_out, size_t lens_cap)
+{
+	if (!path || !st || !ri || !crc || n_threads < 1 || text_len == 0 || (!first_share && !window)) return VC_EINVAL;
+	vc_file_stats local = {0, 0, 0, 0.0};
+	*ri = vc_range_info{UINT64_MAX, UINT64_MAX, 0, 0, 0};
+	memset(crc, 0, sizeof *crc);
+	const double t0 = mono_now();
+	const int fmt = vc_gz_text_format(path);
+	if (fmt < 0) return VC_EINVAL;
+	const char *ce = getenv("VAFC_GZ_CHUNK");   // test knob: compressed bytes per chunk
+	VcGzParallel *g = vc_gzp_open_share(path, vc_gz_inflate_threads(n_threads), ce ? (uint64_t)atoll(ce) : 0,
+	                                    first_share != 0, start_bit, window, text_len);
+	if (!g) return VC_EIO;
+	const int rc = scan_gz_share_g(g, fmt, k, first_share, window, text_len, block_bases, n_threads, local, ri, crc,
+	                               seq_out, seq_cap, lens_out, lens_cap);
+	local.seconds = mono_now() - t0;
+	*st = local;
+	return rc;
+}
+
+extern "C" int vc_scan_gz_share_held(vc_gz_share *h, int k, int first_share, const uint8_t *window, uint64_t text_len,
+                                     int block_bases, int n_threads, vc_file_stats *st, vc_range_info *ri,
+                                     vc_gz_share_crc *crc, uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out,
+                                     size_t lens_cap)
+{
+	if (!h || !h->g || !st || !ri || !crc || n_threads < 1 || text_len == 0 || (!first_share && !window))
+		return VC_EINVAL;
+	vc_file_stats local = {0, 0, 0, 0.0};
+	*ri = vc_range_info{UINT64_MAX, UINT64_MAX, 0, 0, 0};
+	memset(crc, 0, sizeof *crc);
+	const double t0 = mono_now();
+	if (h->format < 0) return VC_EINVAL;
+	VcGzParallel *g = h->g;
+	h->g = nullptr;   // counted once; scan_gz_share_g closes it
+	if (!vc_gzp_resume_share(g, first_share ? nullptr : window, text_len)) {
+		vc_gzp_close(g);
+		return VC_EINVAL;
+	}
+	const int rc = scan_gz_share_g(g, h->format, k, first_share, window, text_len, block_bases, n_threads, local, ri,
+	                               crc, seq_out, seq_cap, lens_out, lens_cap);
 	local.seconds = mono_now() - t0;
 	*st = local;
 	return rc;

@@ -44,6 +44,7 @@ EXPORTS = (
     "vc_scan_records", "vc_reserve_file_ingest",
     "vc_gz_inflate_parallel", "vc_gz_inflate_zlib", "vc_gz_crc32", "vc_gz_crc32_combine",
     "vc_gz_share_scan", "vc_count_gz_share", "vc_scan_gz_share",
+    "vc_gz_share_open", "vc_count_gz_share_held", "vc_scan_gz_share_held", "vc_gz_share_close",
     "vc_fasta_load", "vc_fasta_count", "vc_fasta_name", "vc_fasta_seq", "vc_fasta_data", "vc_fasta_free",
     "vc_count_candidates", "vc_set_nt4_decode",
     "vc_kc_create", "vc_kc_set_partition", "vc_kc_slots", "vc_kc_histogram", "vc_kc_histogram2",
@@ -169,6 +170,14 @@ def lib():
         "vc_scan_gz_share": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_uint64, P, C.c_uint64, C.c_int, C.c_int,
                                        C.POINTER(FileStats), C.POINTER(RangeInfo), C.POINTER(GzShareCrc),
                                        P, C.c_size_t, P, C.c_size_t]),
+        "vc_gz_share_open": (C.c_int, [C.c_char_p, C.c_uint64, C.c_uint64, C.c_int, C.c_uint64, C.c_uint64,
+                                       C.POINTER(GzShareInfo), P, C.POINTER(P)]),
+        "vc_count_gz_share_held": (C.c_int, [P, P, C.c_int, P, C.c_uint64, C.c_int, C.c_int, C.POINTER(FileStats),
+                                             C.POINTER(RangeInfo), C.POINTER(GzShareCrc)]),
+        "vc_scan_gz_share_held": (C.c_int, [P, C.c_int, C.c_int, P, C.c_uint64, C.c_int, C.c_int,
+                                            C.POINTER(FileStats), C.POINTER(RangeInfo), C.POINTER(GzShareCrc),
+                                            P, C.c_size_t, P, C.c_size_t]),
+        "vc_gz_share_close": (None, [P]),
         "vc_reserve_file_ingest": (C.c_int, [P, C.c_int]),
         "vc_fasta_load": (C.c_int, [C.c_char_p, C.POINTER(P)]),
         "vc_fasta_count": (C.c_int, [P]),
@@ -421,6 +430,19 @@ class KmerMap:
         _ck(rc, "vc_count_gz_share(%s)" % fn)
         return st, ri, cr.as_dict()
 
+    def count_gz_share_held(self, share, first_share: bool, window, text_len: int, block_size: int = 10_000_000,
+                            n_thread: int = 4):
+        """count_gz_share from a held share (vc_count_gz_share_held): the
+        scan's decoded chunks are streamed instead of inflated again.  The
+        share is spent (close it afterwards)."""
+        st, ri, cr = FileStats(), RangeInfo(), GzShareCrc()
+        w = None if window is None else np.ascontiguousarray(window, dtype=np.uint8)
+        rc = lib().vc_count_gz_share_held(self._h, share.handle(), 1 if first_share else 0,
+                                          None if w is None else _ptr(w), text_len, block_size, n_thread,
+                                          C.byref(st), C.byref(ri), C.byref(cr))
+        _ck(rc, "vc_count_gz_share_held")
+        return st, ri, cr.as_dict()
+
     def count_file_range(self, fn: str, begin: int, end: int, block_size: int = 10_000_000,
                          n_thread: int = 4):
         """One rank's byte range [begin, end) of a file (vc_count_file_range):
@@ -626,6 +648,46 @@ def gz_share_scan(fn: str, begin: int, end: int, threads: int = 4, chunk_bytes: 
     return {f: int(getattr(info, f)) for f, _ in info._fields_}, wsym
 
 
+class GzShare:
+    """A held share of a gzip stream (vc_gz_share_open): the scan's decoded
+    chunks, kept for one count of the share.  close() frees them (a count
+    spends the share but the handle still needs closing)."""
+
+    def __init__(self, h):
+        self._h = h
+
+    def handle(self):
+        if not self._h:
+            raise VafcError("gz share already closed")
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().vc_gz_share_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def gz_share_open(fn: str, begin: int, end: int, threads: int = 4, chunk_bytes: int = 0, hold_bytes: int = 0):
+    """vc_gz_share_open: gz_share_scan that keeps the share's decoded chunks
+    (at most hold_bytes of buffers) for the count: (info dict, window
+    symbols, GzShare or None when the share was not kept)."""
+    info = GzShareInfo()
+    wsym = np.zeros(GZ_WSIZE, np.uint16)
+    h = P()
+    rc = lib().vc_gz_share_open(fn.encode(), begin, min(end, NO_OFFSET), threads, chunk_bytes, hold_bytes,
+                                C.byref(info), _ptr(wsym), C.byref(h))
+    if rc == VC_EIO:
+        raise FileNotFoundError(fn)
+    _ck(rc, "vc_gz_share_open(%s)" % fn)
+    return {f: int(getattr(info, f)) for f, _ in info._fields_}, wsym, (GzShare(h.value) if h.value else None)
+
+
 def gz_window_after(wsym: np.ndarray, before: np.ndarray) -> np.ndarray:
     """The 32 KiB of text after a share from its symbols and the 32 KiB
     before it (include/vafc.h: 0x8000 | i is byte i of `before`)."""
@@ -655,6 +717,31 @@ def scan_gz_share(fn: str, k: int, first_share: bool, start_bit: int, window, te
     if rc == VC_EIO:
         raise FileNotFoundError(fn)
     _ck(rc, "vc_scan_gz_share(%s)" % fn)
+    reads = None
+    if with_reads:
+        reads, pos = [], 0
+        for i in range(int(st.seqs)):
+            m = int(lens[i])
+            reads.append(seq[pos:pos + m].tobytes())
+            pos += m
+    return st, ri, cr.as_dict(), reads
+
+
+def scan_gz_share_held(share, k: int, first_share: bool, window, text_len: int, block_size: int = 10_000_000,
+                       threads: int = 4, with_reads: bool = False, cap: int = 0):
+    """Host-only vc_scan_gz_share_held: scan_gz_share from a held share."""
+    st, ri, cr = FileStats(), RangeInfo(), GzShareCrc()
+    w = None if window is None else np.ascontiguousarray(window, dtype=np.uint8)
+    seq = lens = None
+    if with_reads:
+        n = max(cap or 2 * text_len + 4096, 64)
+        seq = np.zeros(n, np.uint8)
+        lens = np.zeros(max(n // 2, 16), np.uint32)
+    rc = lib().vc_scan_gz_share_held(share.handle(), k, 1 if first_share else 0, None if w is None else _ptr(w),
+                                     text_len, block_size, threads, C.byref(st), C.byref(ri), C.byref(cr),
+                                     None if seq is None else _ptr(seq), 0 if seq is None else seq.size,
+                                     None if lens is None else _ptr(lens), 0 if lens is None else lens.size)
+    _ck(rc, "vc_scan_gz_share_held")
     reads = None
     if with_reads:
         reads, pos = [], 0

@@ -274,6 +274,15 @@ class RankCounter:
         coordinates; ok False if the file cannot be opened."""
         raise NotImplementedError
 
+    # host bytes a gzip share's scan may keep for the count (0: the count
+    # inflates the share again); see count_gz_share_held
+    gz_hold_bytes = 0
+
+    def count_gz_share_held(self, share, first_share: bool, window, text_len: int, block: int, threads: int):
+        """count_gz_share from a share whose scan kept its decoded chunks
+        (vafc.h vc_count_gz_share_held): one inflate pass instead of two."""
+        raise NotImplementedError
+
     def save(self):
         """Remember the counts and the k-mer tally (before a split file)."""
         raise NotImplementedError
@@ -316,6 +325,7 @@ class HipRankCounter(RankCounter):
         self.map.bind_outputs(self.counts.data_ptr(), self.tally.data_ptr())
         self.device = self.dev if backend == "nccl" else "cpu"
         self._saved = None
+        self.gz_hold_bytes = gz_hold_budget()
 
     def count_range(self, fn, begin, end, block, threads):
         try:
@@ -329,6 +339,10 @@ class HipRankCounter(RankCounter):
             st, ri, crc = self.map.count_gz_share(fn, first_share, start_bit, window, text_len, block, threads)
         except FileNotFoundError:
             return False, 0, 0, (NO_OFFSET, NO_OFFSET, 0, 0), None
+        return True, st.bases, st.seqs, (ri.first, ri.next, ri.errs, ri.stopped), crc
+
+    def count_gz_share_held(self, share, first_share, window, text_len, block, threads):
+        st, ri, crc = self.map.count_gz_share_held(share, first_share, window, text_len, block, threads)
         return True, st.bases, st.seqs, (ri.first, ri.next, ri.errs, ri.stopped), crc
 
     def save(self):
@@ -514,14 +528,28 @@ def _count_gz_shares(fn, i, size, counter, o, rank, world, err, coll_device):
     failed = False
     info = {"start_bit": NO_OFFSET, "end_bit": NO_OFFSET, "text_len": 0, "ok": 1, "ended": 0}
     wsym = np.zeros(vafc.GZ_WSIZE, np.uint16)
+    hold = int(counter.gz_hold_bytes)
+    share = None
     try:
-        if end > begin:
+        if end > begin and hold > 0:     # one inflate pass: the scan's chunks kept for the count
+            info, wsym, share = vafc.gz_share_open(fn, begin, end, threads=o["t"], hold_bytes=hold)
+        elif end > begin:
             info, wsym = vafc.gz_share_scan(fn, begin, end, threads=o["t"])
     except FileNotFoundError:
         info["ok"] = 0
     except Exception as e:
         err("Error: counting failed on %s (%s)\n" % (fn, e))
         failed = True
+    try:
+        return _count_gz_share_scanned(fn, i, counter, o, rank, world, err, coll_device, info, wsym, share, failed)
+    finally:
+        if share is not None:
+            share.close()
+
+
+def _count_gz_share_scanned(fn, i, counter, o, rank, world, err, coll_device, info, wsym, share, failed):
+    """_count_gz_shares after this rank's scan (share: its held chunks, or None)."""
+    import vafc
     rows = allgather_ints([info["start_bit"], info["end_bit"], info["text_len"], info["ok"], info["ended"],
                            1 if failed else 0], world, coll_device)
     if any(r[5] for r in rows):
@@ -545,8 +573,12 @@ def _count_gz_shares(fn, i, size, counter, o, rank, world, err, coll_device):
     good, b, s, rinfo, crc = True, 0, 0, (EMPTY_RANGE, EMPTY_RANGE, 0, 0), None
     if int(rows[rank][0]) != NO_OFFSET:
         try:
-            good, b, s, rinfo, crc = counter.count_gz_share(fn, rank == 0, int(rows[rank][0]), windows[rank],
-                                                            int(rows[rank][2]), o["b"], o["t"])
+            if share is not None:
+                good, b, s, rinfo, crc = counter.count_gz_share_held(share, rank == 0, windows[rank],
+                                                                     int(rows[rank][2]), o["b"], o["t"])
+            else:
+                good, b, s, rinfo, crc = counter.count_gz_share(fn, rank == 0, int(rows[rank][0]), windows[rank],
+                                                                int(rows[rank][2]), o["b"], o["t"])
         except Exception as e:
             err("Error: counting failed on %s (%s)\n" % (fn, e))
             failed = True
@@ -561,6 +593,28 @@ def _count_gz_shares(fn, i, size, counter, o, rank, world, err, coll_device):
         return good, b, s, 0, True
     counter.restore()
     return whole()
+
+
+def gz_hold_budget() -> int:
+    """Host bytes one rank's gzip share may keep between its scan and its
+    count ($VAFC_GZ_HOLD, bytes; 0 turns holding off): by default a quarter
+    of the available memory split over this node's ranks, at most 32 GiB.  A
+    held share takes about 3-4 bytes per byte of text (16-bit symbols and the
+    resolved text); a share over the budget is inflated again, as before."""
+    env = os.environ.get("VAFC_GZ_HOLD")
+    if env is not None:
+        return max(int(env), 0)
+    avail = 0
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    avail = int(line.split()[1]) * 1024
+                    break
+    except OSError:
+        return 0
+    local_world = max(int(os.environ.get("LOCAL_WORLD_SIZE", "1")), 1)
+    return min(avail // (4 * local_world), 32 << 30)
 
 
 def rank_device(local: int, local_world: int, n_dev: int, backend: str, rehearsal: bool):

@@ -303,36 +303,113 @@ def test_parallel_parse_of_gzip_stops_early_without_reading_on(tmp_path, monkeyp
 # in one process: every share's reads in order == the sequential reader's
 # --------------------------------------------------------------------------
 
-def _shares(path, world, k=5, block=100, chunk=16 << 10, threads=3):
+def _shares(path, world, k=5, block=100, chunk=16 << 10, threads=3, hold=0, held_out=None):
     """Scan, chain and count the `world` shares of a gzip file; returns
-    (chained, ranges, crcs, reads in share order)."""
+    (chained, ranges, crcs, reads in share order).  hold > 0: the scans keep
+    their decoded chunks (vc_gz_share_open) and the counts resume from them
+    (vc_scan_gz_share_held) where a share fitted the budget; held_out collects
+    which shares did."""
     import vafc
     import vafc_dist as D
     size = os.path.getsize(path)
-    rows, wsyms = [], []
-    for r in range(world):
-        b, e = D.byte_range(size, r, world)
-        if e <= b:
-            rows.append((D.NO_OFFSET, D.NO_OFFSET, 0, 1, 0))
-            wsyms.append(np.zeros(vafc.GZ_WSIZE, np.uint16))
-            continue
-        info, w = vafc.gz_share_scan(path, b, e, threads=threads, chunk_bytes=chunk)
-        rows.append((info["start_bit"], info["end_bit"], info["text_len"], info["ok"], info["ended"]))
-        wsyms.append(w)
-    if not D.gz_shares_chain(rows):
-        return False, None, None, None
-    wins = D.gz_windows(rows, wsyms)
-    ranges, crcs, reads = [], [], []
-    for r in range(world):
-        if rows[r][0] == D.NO_OFFSET:
-            ranges.append((D.EMPTY_RANGE, D.EMPTY_RANGE, 0, 0))
-            continue
-        st, ri, cr, rd = vafc.scan_gz_share(path, k, r == 0, rows[r][0], wins[r], rows[r][2], block, threads,
-                                            with_reads=True)
-        ranges.append((ri.first, ri.next, ri.errs, ri.stopped))
-        crcs.append(cr)
-        reads += rd
-    return True, ranges, crcs, reads
+    rows, wsyms, held = [], [], []
+    try:
+        for r in range(world):
+            b, e = D.byte_range(size, r, world)
+            if e <= b:
+                rows.append((D.NO_OFFSET, D.NO_OFFSET, 0, 1, 0))
+                wsyms.append(np.zeros(vafc.GZ_WSIZE, np.uint16))
+                held.append(None)
+                continue
+            if hold:
+                info, w, h = vafc.gz_share_open(path, b, e, threads=threads, chunk_bytes=chunk, hold_bytes=hold)
+            else:
+                (info, w), h = vafc.gz_share_scan(path, b, e, threads=threads, chunk_bytes=chunk), None
+            rows.append((info["start_bit"], info["end_bit"], info["text_len"], info["ok"], info["ended"]))
+            wsyms.append(w)
+            held.append(h)
+        if held_out is not None:
+            held_out += [h is not None for h in held]
+        if not D.gz_shares_chain(rows):
+            return False, None, None, None
+        wins = D.gz_windows(rows, wsyms)
+        ranges, crcs, reads = [], [], []
+        for r in range(world):
+            if rows[r][0] == D.NO_OFFSET:
+                ranges.append((D.EMPTY_RANGE, D.EMPTY_RANGE, 0, 0))
+                continue
+            if held[r] is not None:
+                st, ri, cr, rd = vafc.scan_gz_share_held(held[r], k, r == 0, wins[r], rows[r][2], block, threads,
+                                                         with_reads=True)
+            else:
+                st, ri, cr, rd = vafc.scan_gz_share(path, k, r == 0, rows[r][0], wins[r], rows[r][2], block,
+                                                    threads, with_reads=True)
+            ranges.append((ri.first, ri.next, ri.errs, ri.stopped))
+            crcs.append(cr)
+            reads += rd
+        return True, ranges, crcs, reads
+    finally:
+        for h in held:
+            if h is not None:
+                h.close()
+
+
+def _share_file(p, text, shape):
+    if shape == "one":
+        data = _member(text, level=1)
+    elif shape == "pigz":      # sync-flushed pieces: empty stored blocks between them
+        c = zlib.compressobj(1, zlib.DEFLATED, -15)
+        body = b"".join(c.compress(text[a:a + 60000]) + c.flush(zlib.Z_SYNC_FLUSH)
+                        for a in range(0, len(text), 60000)) + c.flush()
+        data = b"\x1f\x8b\x08\x00\x00\x00\x00\x00\x04\x03" + body + struct.pack("<II", zlib.crc32(text), len(text))
+    elif shape == "multi":     # members cut inside records
+        cut = [0, len(text) // 3 + 11, 2 * len(text) // 3 + 5, len(text)]
+        data = b"".join(_member(text[a:b], level=1) for a, b in zip(cut, cut[1:]))
+    else:                      # fixed-Huffman blocks only: no later share can start blind,
+        data = _member(text, level=1, strategy=zlib.Z_FIXED)   # so share 0 decodes to the end
+    with open(p, "wb") as f:
+        f.write(data)
+
+
+@pytest.mark.parametrize("shape", ["one", "pigz", "multi", "fixed_blocks"])
+@pytest.mark.parametrize("hold", [1 << 30, 1, 4 << 20])
+@pytest.mark.parametrize("world", [2, 3])
+def test_gzip_held_shares_reproduce_the_stream(tmp_path, text, shape, hold, world):
+    """The single-pass shares (vc_gz_share_open + vc_scan_gz_share_held): a
+    share that fits the budget is counted from the scan's own decoded chunks
+    (and zlib past its end for the last record), one that does not is
+    decoded again -- the reads, ranges and CRC chain are the two-pass ones."""
+    import vafc
+    import vafc_dist as D
+    p = str(tmp_path / "h.fq.gz")
+    _share_file(p, text, shape)
+    kept = []
+    chained, ranges, crcs, reads = _shares(p, world, hold=hold, held_out=kept)
+    assert chained
+    if hold == 1:
+        assert not any(kept)
+    elif hold == 4 << 20:      # a chunk's buffers take 3 MiB at least: the budget runs out mid-scan
+        assert not all(kept)
+    elif shape != "fixed_blocks":
+        assert all(kept)
+    st0, r0 = vafc.scan_file(p, 5, 100, with_reads=True)
+    assert reads == r0
+    assert D.chain_holds(ranges)
+    assert D.gz_crc_chain(crcs, vafc.gz_crc32_combine)
+
+
+def test_gzip_held_share_closed_unused(tmp_path, text):
+    """A held share closed without a count (another rank's share failed):
+    the decoder's threads and buffers go with it."""
+    import vafc
+    p = str(tmp_path / "u.fq.gz")
+    _share_file(p, text, "one")
+    size = os.path.getsize(p)
+    for _ in range(3):
+        info, w, h = vafc.gz_share_open(p, size // 2, size, threads=3, chunk_bytes=16 << 10, hold_bytes=1 << 30)
+        assert info["ok"] and h is not None
+        h.close()
+        h.close()
 
 
 @pytest.mark.parametrize("shape", ["one", "pigz", "multi", "fixed_blocks"])

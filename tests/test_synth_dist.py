@@ -156,7 +156,7 @@ def _driver_rank(rank, world, port, argv, cwd, out_json, counter):
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     os.chdir(cwd)
     lines = []
-    calls = {"ranges": 0, "whole": 0, "restores": 0, "gz_shares": 0}
+    calls = {"ranges": 0, "whole": 0, "restores": 0, "gz_shares": 0, "gz_held": 0}
 
     class OracleRankCounter(D.RankCounter):     # CPU stand-in for the per-GPU counter (test infrastructure)
         """The oracle counts what the product's host-only range reader
@@ -194,6 +194,9 @@ def _driver_rank(rank, world, port, argv, cwd, out_json, counter):
                 self.km += km
             return True, st.bases, st.seqs, (ri.first, ri.next, ri.errs, ri.stopped)
 
+        # the held (single-pass) shares on odd-sized worlds, the two-pass ones on even
+        gz_hold_bytes = (1 << 30) if world % 2 else 0
+
         def count_gz_share(self, fn, first_share, start_bit, window, text_len, block, threads):
             import vafc
             calls["gz_shares"] += 1
@@ -202,6 +205,17 @@ def _driver_rank(rank, world, port, argv, cwd, out_json, counter):
                                                         threads, with_reads=True)
             except FileNotFoundError:
                 return False, 0, 0, (D.NO_OFFSET, D.NO_OFFSET, 0, 0), None
+            return self._add(st, ri, crc, reads)
+
+        def count_gz_share_held(self, share, first_share, window, text_len, block, threads):
+            import vafc
+            calls["gz_shares"] += 1
+            calls["gz_held"] += 1
+            st, ri, crc, reads = vafc.scan_gz_share_held(share, self.k, first_share, window, text_len, block,
+                                                         threads, with_reads=True)
+            return self._add(st, ri, crc, reads)
+
+        def _add(self, st, ri, crc, reads):
             if reads:
                 lens = np.array([len(r) for r in reads], np.uint32)
                 offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
@@ -297,6 +311,8 @@ def test_dist_driver_matches_reference(name, world, counter, manifest, synth_dir
         if name in DIST_GZ_CLEAN:   # every gzip file split into shares: nothing counted whole, nothing redone
             assert all(c["restores"] == 0 and c["whole"] == 0 for c in calls), calls
             assert sum(c["gz_shares"] for c in calls) >= (world if name != "edge_gz" else 1), calls
+            # odd worlds hold their scans' chunks: every share counted in one pass
+            assert sum(c["gz_held"] for c in calls) == (sum(c["gz_shares"] for c in calls) if world % 2 else 0)
         if name.startswith("mal_") or name == "truncated":
             assert all(c["restores"] >= 1 for c in calls), calls
 
@@ -328,3 +344,4 @@ def test_dist_driver_gzip_bad_crc_falls_back(world, manifest, synth_dir, tmp_pat
     assert data == data1 and stats == stats1
     assert all(c["restores"] >= 1 for c in calls), calls
     assert sum(c["whole"] for c in calls) == 1 and sum(c["gz_shares"] for c in calls) >= 2, calls
+    assert sum(c["gz_held"] for c in calls) == (sum(c["gz_shares"] for c in calls) if world % 2 else 0)

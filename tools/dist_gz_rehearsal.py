@@ -26,8 +26,10 @@ sys.path.insert(0, os.path.join(ROOT, "kmer-cnt_amd"))
 DRIVER = os.path.join(ROOT, "kmer-cnt_amd", "vafc_dist.py")
 
 
-def run(n, threads, pat, gz, out, timeout=600):
+def run(n, threads, pat, gz, out, timeout=600, hold=None):
     env = dict(os.environ, VAFC_DIST_BACKEND="gloo", VAFC_REHEARSAL="1")
+    if hold is not None:
+        env["VAFC_GZ_HOLD"] = str(hold)
     argv = ["-v", "-k", "21", "-t", str(threads), "-p", pat, "-o", out, gz]
     t0 = time.time()
     if n == 1:
@@ -99,20 +101,24 @@ def main():
                                                                                 text / 1e9),
            "box": "one GPU box, %d reader threads in all: 1 rank x %d against %d ranks x %d (gloo, every rank on "
                   "GPU 0)" % (a.threads, a.threads, a.ranks, max(1, a.threads // a.ranks)),
-           "runs": {"1": [], str(a.ranks): []}}
+           "runs": {"1": [], str(a.ranks): [], "%d_two_pass" % a.ranks: []}}
     md5s = {}
     run(1, a.threads, pat, gz, os.path.join(tmp, "warm.vaf"))
     for rep in range(a.rounds):
-        for n in (1, a.ranks):
-            o = os.path.join(tmp, "r%d.vaf" % n)
-            r = run(n, max(1, a.threads // n), pat, gz, o)
-            md5s[n] = bench.md5(o)
-            out["runs"][str(n)].append(r)
-            sys.stderr.write("[gzr] %d rank(s), round %d: %.1f Mbases/s\n" % (n, rep + 1, r["mbases"]))
-    out["vaf_identical"] = md5s[1] == md5s[a.ranks]
-    out["note"] = ("the split-gzip pass decodes each share twice (a blind scan for the window chain, then the "
-                   "counting pass), so at a fixed CPU share N ranks do about twice the single rank's inflate "
-                   "work; with a CPU share per rank (one per GPU) the pass takes about 2/N of the single rank's")
+        # N ranks with the scans' chunks held for the count (one inflate pass,
+        # the driver's default budget) and with holding off (VAFC_GZ_HOLD=0:
+        # every share inflated twice)
+        for n, hold, key in ((1, None, "1"), (a.ranks, None, str(a.ranks)),
+                             (a.ranks, 0, "%d_two_pass" % a.ranks)):
+            o = os.path.join(tmp, "r%s.vaf" % key)
+            r = run(n, max(1, a.threads // n), pat, gz, o, hold=hold)
+            md5s[key] = bench.md5(o)
+            out["runs"][key].append(r)
+            sys.stderr.write("[gzr] %s rank(s), round %d: %.1f Mbases/s\n" % (key, rep + 1, r["mbases"]))
+    out["vaf_identical"] = len(set(md5s.values())) == 1
+    out["note"] = ("held shares: each rank's blind scan keeps its decoded chunks and the count streams them, so a "
+                   "share is inflated once; two_pass: the scan's output is dropped and the count inflates the "
+                   "share again from its start bit with the known window")
     print(json.dumps(out))
     os.unlink(gz)
     if work != tmp:
