@@ -358,16 +358,20 @@ int vc_scan_gz_share(const char *path, int k, int first_share, uint64_t start_bi
                      vc_gz_share_crc *crc, uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out, size_t lens_cap);
 
 /* One pass per share instead of two: vc_gz_share_open scans as
- * vc_gz_share_scan and keeps the share's decoded chunks (about 3 bytes of
- * buffers per byte of text, at most hold_bytes), so that the count resolves
- * them with the window instead of inflating the share again.  *held is NULL
- * when the share did not fit in hold_bytes (or could not be scanned): the
- * caller then counts with vc_count_gz_share.  A held share is counted once
- * (vc_count_gz_share_held / vc_scan_gz_share_held, same outputs as the
- * unheld forms) and closed with vc_gz_share_close. */
+ * vc_gz_share_scan and keeps the share's decoded chunks (about one byte of
+ * memory per byte of text -- two per symbol for the start of each chunk,
+ * until its references to the unknown window run out -- at most hold_bytes),
+ * so that the count resolves them with the window instead of inflating the
+ * share again.  *held is NULL when the share did not fit in hold_bytes (or
+ * could not be scanned): the caller then counts with vc_count_gz_share.  A
+ * held share is counted once (vc_count_gz_share_held / vc_scan_gz_share_held,
+ * same outputs as the unheld forms) and closed with vc_gz_share_close.  ctx:
+ * the counter that will count the share (the scan's threads run on its GPU's
+ * NUMA node, where the kept text is then read), or NULL. */
 typedef struct vc_gz_share vc_gz_share;
-int vc_gz_share_open(const char *path, uint64_t begin, uint64_t end, int n_threads, uint64_t chunk_bytes,
-                     uint64_t hold_bytes, vc_gz_share_info *out, uint16_t *window_sym, vc_gz_share **held);
+int vc_gz_share_open(vc_ctx *ctx, const char *path, uint64_t begin, uint64_t end, int n_threads,
+                     uint64_t chunk_bytes, uint64_t hold_bytes, vc_gz_share_info *out, uint16_t *window_sym,
+                     vc_gz_share **held);
 int vc_count_gz_share_held(vc_ctx *ctx, vc_gz_share *held, int first_share, const uint8_t *window, uint64_t text_len,
                            int block_bases, int n_threads, vc_file_stats *st, vc_range_info *ri, vc_gz_share_crc *crc);
 int vc_scan_gz_share_held(vc_gz_share *held, int k, int first_share, const uint8_t *window, uint64_t text_len,

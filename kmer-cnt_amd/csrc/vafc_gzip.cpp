@@ -1261,6 +1261,10 @@ void VcGzParallel::worker()
 			{
 				const double r0 = gz_now();
 				resolve(*task);
+				// a resumed share's chunk is never decoded again: its symbols and the
+				// buffer the piece swapped in go now, spread over the workers, rather
+				// than all at once when the share is closed
+				if (continue_after_) task->src->out.release_buffers();
 				const double r1 = gz_now();
 				piece_crcs(*task);
 				prof_resolve_us += (uint64_t)((r1 - r0) * 1e6);
@@ -1876,7 +1880,12 @@ void vc_gzp_release(VcGzParallel *g, void *hold) { g->release(hold); }
 
 void vc_gzp_stats(VcGzParallel *g, VcGzStats *st) { g->get_stats(st); }
 
-void vc_gzp_close(VcGzParallel *g) { delete g; }
+void vc_gzp_close(VcGzParallel *g)
+{
+	const double t0 = gz_now();
+	delete g;
+	if (getenv("VAFC_GZ_PROFILE")) fprintf(stderr, "[gzp] close %.3f s\n", gz_now() - t0);
+}
 
 bool vc_gzp_scan_share(const char *path, int threads, uint64_t chunk_bytes, uint64_t begin, uint64_t end,
                        VcGzShare *sh, uint16_t *window_sym)
@@ -1993,30 +2002,6 @@ extern "C" uint32_t vc_gz_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t l
 }
 
 int vc_gz_text_format(const char *path);   // vafc_ingest.cpp
-
-extern "C" int vc_gz_share_open(const char *path, uint64_t begin, uint64_t end, int n_threads, uint64_t chunk_bytes,
-                                uint64_t hold_bytes, vc_gz_share_info *out, uint16_t *window_sym, vc_gz_share **held)
-{
-	if (!path || !out || !held || end <= begin) return VC_EINVAL;
-	*held = nullptr;
-	const int t = n_threads < 1 ? 1 : n_threads;
-	VcGzShare sh;
-	VcGzParallel *g = nullptr;
-	if (!vc_gzp_scan_share_hold(path, t, chunk_bytes, begin, end, hold_bytes, &sh, window_sym, &g)) return VC_EIO;
-	out->start_bit = sh.start_bit;
-	out->end_bit = sh.end_bit;
-	out->text_len = sh.text_len;
-	out->ok = sh.ok ? 1u : 0u;
-	out->ended = sh.start_bit != UINT64_MAX && sh.end_bit == UINT64_MAX ? 1u : 0u;
-	if (g) {
-		vc_gz_share *h = new vc_gz_share;
-		h->g = g;
-		h->format = vc_gz_text_format(path);
-		h->threads = t;
-		*held = h;
-	}
-	return VC_OK;
-}
 
 extern "C" void vc_gz_share_close(vc_gz_share *h)
 {

@@ -1621,11 +1621,10 @@ extern "C" int vc_count_file_range(vc_ctx *c, const char *path, uint64_t begin, 
 // the share's first block with its known window, or a held share resumed),
 // the parallel reader over the share's text as a range (plus the previous
 // byte, for the first guess).  Takes g and closes it.
-static int count_gz_share_g(vc_ctx *c, VcGzParallel *g, int fmt, int t, int first_share, const uint8_t *window,
-                            uint64_t text_len, int block_bases, vc_file_stats &local, vc_range_info *ri,
-                            vc_gz_share_crc *crc)
+static int count_gz_share_g(vc_ctx *c, VcGzParallel *g, int fmt, int parsers, int first_share,
+                            const uint8_t *window, uint64_t text_len, int block_bases, vc_file_stats &local,
+                            vc_range_info *ri, vc_gz_share_crc *crc)
 {
-	const int parsers = vc_gz_parse_threads(t);
 	int rc = reserve_ingest(c, parsers, false);
 	VcTextRange R;
 	const size_t np = first_share ? 0 : 1;
@@ -1669,10 +1668,46 @@ extern "C" int vc_count_gz_share(vc_ctx *c, const char *path, int first_share, u
 	VcGzParallel *g = vc_gzp_open_share(path, vc_gz_inflate_threads(t), ce ? (uint64_t)atoll(ce) : 0,
 	                                    first_share != 0, start_bit, window, text_len);
 	if (!g) return VC_EIO;
-	const int rc = count_gz_share_g(c, g, fmt, t, first_share, window, text_len, block_bases, local, ri, crc);
+	const int rc = count_gz_share_g(c, g, fmt, vc_gz_parse_threads(t), first_share, window, text_len, block_bases,
+	                                local, ri, crc);
 	local.seconds = wall_now() - t0;
 	if (st) *st = local;
 	return rc;
+}
+
+int vc_gz_text_format(const char *path);   // vafc_ingest.cpp
+
+extern "C" int vc_gz_share_open(vc_ctx *c, const char *path, uint64_t begin, uint64_t end, int n_threads,
+                                uint64_t chunk_bytes, uint64_t hold_bytes, vc_gz_share_info *out,
+                                uint16_t *window_sym, vc_gz_share **held)
+{
+	if (!path || !out || !held || end <= begin) return VC_EINVAL;
+	*held = nullptr;
+	const int t = n_threads < 1 ? 1 : n_threads;
+	// the scan's threads where the count's will run (the GPU's NUMA node):
+	// the chunks they keep are first touched there, so the count reads them
+	// from local memory
+	VcCpuSet none;
+	CPU_ZERO(&none.set);
+	if (c) HIPCK(hipSetDevice(c->dev));
+	const int ct = clamp_threads(t);
+	VcAffinityScope placement(c ? gpu_cpus(c, vc_gz_inflate_threads(ct) + vc_gz_parse_threads(ct) + 2) : none);
+	VcGzShare sh;
+	VcGzParallel *g = nullptr;
+	if (!vc_gzp_scan_share_hold(path, t, chunk_bytes, begin, end, hold_bytes, &sh, window_sym, &g)) return VC_EIO;
+	out->start_bit = sh.start_bit;
+	out->end_bit = sh.end_bit;
+	out->text_len = sh.text_len;
+	out->ok = sh.ok ? 1u : 0u;
+	out->ended = sh.start_bit != UINT64_MAX && sh.end_bit == UINT64_MAX ? 1u : 0u;
+	if (g) {
+		vc_gz_share *h = new vc_gz_share;
+		h->g = g;
+		h->format = vc_gz_text_format(path);
+		h->threads = t;
+		*held = h;
+	}
+	return VC_OK;
 }
 
 extern "C" int vc_count_gz_share_held(vc_ctx *c, vc_gz_share *h, int first_share, const uint8_t *window,
@@ -1694,7 +1729,8 @@ extern "C" int vc_count_gz_share_held(vc_ctx *c, vc_gz_share *h, int first_share
 		vc_gzp_close(g);
 		return VC_EINVAL;
 	}
-	const int rc = count_gz_share_g(c, g, h->format, t, first_share, window, text_len, block_bases, local, ri, crc);
+	const int rc = count_gz_share_g(c, g, h->format, vc_gz_held_parse_threads(t), first_share, window, text_len,
+	                                block_bases, local, ri, crc);
 	local.seconds = wall_now() - t0;
 	if (st) *st = local;
 	return rc;

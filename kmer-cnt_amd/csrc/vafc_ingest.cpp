@@ -1054,13 +1054,12 @@ extern "C" int vc_scan_file_range(const char *path, int k, int block_bases, int 
 
 // The host-only count of one gzip share from an open inflater (closed here).
 static int scan_gz_share_g(VcGzParallel *g, int fmt, int k, int first_share, const uint8_t *window, uint64_t text_len,
-                           int block_bases, int n_threads, vc_file_stats &local, vc_range_info *ri,
+                           int block_bases, int parsers, vc_file_stats &local, vc_range_info *ri,
                            vc_gz_share_crc *crc, uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out,
                            size_t lens_cap)
 {
 	const char *pe = getenv("VAFC_INGEST_PIECE");
 	const uint64_t piece = pe && atoll(pe) >= 2 ? (uint64_t)atoll(pe) : ((uint64_t)16 << 20);
-	const int parsers = vc_gz_parse_threads(n_threads);
 	HostSink sink(parsers + 2, piece, seq_out, seq_cap, lens_out, lens_cap);
 	const size_t np = first_share ? 0 : 1;
 	VcTextRange R;
@@ -1095,8 +1094,9 @@ extern "C" int vc_scan_gz_share(const char *path, int k, int first_share, uint64
 	VcGzParallel *g = vc_gzp_open_share(path, vc_gz_inflate_threads(n_threads), ce ? (uint64_t)atoll(ce) : 0,
 	                                    first_share != 0, start_bit, window, text_len);
 	if (!g) return VC_EIO;
-	const int rc = scan_gz_share_g(g, fmt, k, first_share, window, text_len, block_bases, n_threads, local, ri, crc,
-	                               seq_out, seq_cap, lens_out, lens_cap);
+	const int rc = scan_gz_share_g(g, fmt, k, first_share, window, text_len, block_bases,
+	                               vc_gz_parse_threads(n_threads), local, ri, crc, seq_out, seq_cap, lens_out,
+	                               lens_cap);
 	local.seconds = mono_now() - t0;
 	*st = local;
 	return rc;
@@ -1120,8 +1120,9 @@ extern "C" int vc_scan_gz_share_held(vc_gz_share *h, int k, int first_share, con
 		vc_gzp_close(g);
 		return VC_EINVAL;
 	}
-	const int rc = scan_gz_share_g(g, h->format, k, first_share, window, text_len, block_bases, n_threads, local, ri,
-	                               crc, seq_out, seq_cap, lens_out, lens_cap);
+	const int rc = scan_gz_share_g(g, h->format, k, first_share, window, text_len, block_bases,
+	                               vc_gz_held_parse_threads(n_threads), local, ri, crc, seq_out, seq_cap, lens_out,
+	                               lens_cap);
 	local.seconds = mono_now() - t0;
 	*st = local;
 	return rc;

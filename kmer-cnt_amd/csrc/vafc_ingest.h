@@ -157,6 +157,15 @@ inline int vc_gz_parse_threads(int threads)
 	const int n = e && atoi(e) > 0 ? atoi(e) : (threads + 3) / 5;
 	return n < 1 ? 1 : n;
 }
+// Parse workers for a held gzip share (vc_count_gz_share_held): its chunks
+// are already inflated, so the parse takes the inflaters' place: -t of them
+// ($VAFC_GZ_PARSERS overrides, as above).
+inline int vc_gz_held_parse_threads(int threads)
+{
+	const char *e = getenv("VAFC_GZ_PARSERS");
+	const int n = e && atoi(e) > 0 ? atoi(e) : threads;
+	return n < 1 ? 1 : n;
+}
 // Inflate workers for gzip input: -t of them, next to the parse workers
 // (measured on a 16-CPU share: 16 inflate + 3 parse workers beat 13 + 3 and
 // 11 + 3, profiles/r02_gz_sweep3.log); $VAFC_GZ_INFLATERS overrides.

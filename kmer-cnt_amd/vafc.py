@@ -170,7 +170,7 @@ def lib():
         "vc_scan_gz_share": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_uint64, P, C.c_uint64, C.c_int, C.c_int,
                                        C.POINTER(FileStats), C.POINTER(RangeInfo), C.POINTER(GzShareCrc),
                                        P, C.c_size_t, P, C.c_size_t]),
-        "vc_gz_share_open": (C.c_int, [C.c_char_p, C.c_uint64, C.c_uint64, C.c_int, C.c_uint64, C.c_uint64,
+        "vc_gz_share_open": (C.c_int, [P, C.c_char_p, C.c_uint64, C.c_uint64, C.c_int, C.c_uint64, C.c_uint64,
                                        C.POINTER(GzShareInfo), P, C.POINTER(P)]),
         "vc_count_gz_share_held": (C.c_int, [P, P, C.c_int, P, C.c_uint64, C.c_int, C.c_int, C.POINTER(FileStats),
                                              C.POINTER(RangeInfo), C.POINTER(GzShareCrc)]),
@@ -673,14 +673,16 @@ class GzShare:
             pass
 
 
-def gz_share_open(fn: str, begin: int, end: int, threads: int = 4, chunk_bytes: int = 0, hold_bytes: int = 0):
+def gz_share_open(fn: str, begin: int, end: int, threads: int = 4, chunk_bytes: int = 0, hold_bytes: int = 0,
+                  kmap=None):
     """vc_gz_share_open: gz_share_scan that keeps the share's decoded chunks
     (at most hold_bytes of buffers) for the count: (info dict, window
-    symbols, GzShare or None when the share was not kept)."""
+    symbols, GzShare or None when the share was not kept).  kmap: the
+    KmerMap that will count the share (its GPU's NUMA node), or None."""
     info = GzShareInfo()
     wsym = np.zeros(GZ_WSIZE, np.uint16)
     h = P()
-    rc = lib().vc_gz_share_open(fn.encode(), begin, min(end, NO_OFFSET), threads, chunk_bytes, hold_bytes,
+    rc = lib().vc_gz_share_open(None if kmap is None else kmap._h, fn.encode(), begin, min(end, NO_OFFSET), threads, chunk_bytes, hold_bytes,
                                 C.byref(info), _ptr(wsym), C.byref(h))
     if rc == VC_EIO:
         raise FileNotFoundError(fn)

@@ -283,6 +283,10 @@ class RankCounter:
         (vafc.h vc_count_gz_share_held): one inflate pass instead of two."""
         raise NotImplementedError
 
+    def gz_kmap(self):
+        """The vafc.KmerMap a held share's scan is placed for (None: no placement)."""
+        return None
+
     def save(self):
         """Remember the counts and the k-mer tally (before a split file)."""
         raise NotImplementedError
@@ -340,6 +344,9 @@ class HipRankCounter(RankCounter):
         except FileNotFoundError:
             return False, 0, 0, (NO_OFFSET, NO_OFFSET, 0, 0), None
         return True, st.bases, st.seqs, (ri.first, ri.next, ri.errs, ri.stopped), crc
+
+    def gz_kmap(self):
+        return self.map
 
     def count_gz_share_held(self, share, first_share, window, text_len, block, threads):
         st, ri, crc = self.map.count_gz_share_held(share, first_share, window, text_len, block, threads)
@@ -532,7 +539,8 @@ def _count_gz_shares(fn, i, size, counter, o, rank, world, err, coll_device):
     share = None
     try:
         if end > begin and hold > 0:     # one inflate pass: the scan's chunks kept for the count
-            info, wsym, share = vafc.gz_share_open(fn, begin, end, threads=o["t"], hold_bytes=hold)
+            info, wsym, share = vafc.gz_share_open(fn, begin, end, threads=o["t"], hold_bytes=hold,
+                                                   kmap=counter.gz_kmap())
         elif end > begin:
             info, wsym = vafc.gz_share_scan(fn, begin, end, threads=o["t"])
     except FileNotFoundError:

@@ -59,17 +59,21 @@ def one(gz, world, threads, hold):
     assert D.gz_shares_chain(rows)
     wins = D.gz_windows(rows, ws)
     bases, ranges = 0, []
+    close_s = 0.0
     for r in range(world):
         if hs[r] is not None:
             st, ri, _, _ = vafc.scan_gz_share_held(hs[r], 21, r == 0, wins[r], rows[r][2], 10_000_000, threads)
+            tc = time.time()
             hs[r].close()
+            close_s += time.time() - tc
         else:
             st, ri, _, _ = vafc.scan_gz_share(gz, 21, r == 0, rows[r][0], wins[r], rows[r][2], 10_000_000, threads)
         bases += st.bases
         ranges.append((ri.first, ri.next, ri.errs, ri.stopped))
     t2 = time.time()
     assert D.chain_holds(ranges)
-    return {"scan_s": round(t1 - t0, 3), "count_s": round(t2 - t1, 3), "bases": int(bases),
+    return {"scan_s": round(t1 - t0, 3), "count_s": round(t2 - t1, 3), "close_s": round(close_s, 3),
+            "bases": int(bases),
             "held": [h is not None for h in hs]}
 
 
