@@ -358,9 +358,10 @@ int vc_scan_gz_share(const char *path, int k, int first_share, uint64_t start_bi
                      vc_gz_share_crc *crc, uint8_t *seq_out, size_t seq_cap, uint32_t *lens_out, size_t lens_cap);
 
 /* One pass per share instead of two: vc_gz_share_open scans as
- * vc_gz_share_scan and keeps the share's decoded chunks (about one byte of
- * memory per byte of text -- two per symbol for the start of each chunk,
- * until its references to the unknown window run out -- at most hold_bytes),
+ * vc_gz_share_scan and keeps the share's decoded chunks (one to two bytes of
+ * memory per byte of text: two for every symbol decoded while the chunk can
+ * still refer to the unknown window, which in FASTQ is most of it; at most
+ * hold_bytes),
  * so that the count resolves them with the window instead of inflating the
  * share again.  *held is NULL when the share did not fit in hold_bytes (or
  * could not be scanned): the caller then counts with vc_count_gz_share.  A

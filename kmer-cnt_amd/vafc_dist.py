@@ -607,8 +607,8 @@ def gz_hold_budget() -> int:
     """Host bytes one rank's gzip share may keep between its scan and its
     count ($VAFC_GZ_HOLD, bytes; 0 turns holding off): by default a quarter
     of the available memory split over this node's ranks, at most 32 GiB.  A
-    held share takes about 3-4 bytes per byte of text (16-bit symbols and the
-    resolved text); a share over the budget is inflated again, as before."""
+    held share takes about 2 bytes per byte of FASTQ text (16-bit symbols,
+    profiles/r06k_held.json); a share over the budget is inflated again."""
     env = os.environ.get("VAFC_GZ_HOLD")
     if env is not None:
         return max(int(env), 0)

@@ -56,10 +56,18 @@ def one(gz, world, threads, hold):
         ws.append(w)
         hs.append(h)
     t1 = time.time()
+    mem = {}
+    try:   # how much of the kept text sits on huge pages
+        for line in open("/proc/self/smaps_rollup"):
+            if line.split(":")[0] in ("Rss", "AnonHugePages"):
+                mem[line.split(":")[0]] = int(line.split()[1]) >> 10
+    except OSError:
+        pass
     assert D.gz_shares_chain(rows)
     wins = D.gz_windows(rows, ws)
     bases, ranges = 0, []
     close_s = 0.0
+    profs = []
     for r in range(world):
         if hs[r] is not None:
             st, ri, _, _ = vafc.scan_gz_share_held(hs[r], 21, r == 0, wins[r], rows[r][2], 10_000_000, threads)
@@ -70,11 +78,15 @@ def one(gz, world, threads, hold):
             st, ri, _, _ = vafc.scan_gz_share(gz, 21, r == 0, rows[r][0], wins[r], rows[r][2], 10_000_000, threads)
         bases += st.bases
         ranges.append((ri.first, ri.next, ri.errs, ri.stopped))
+        prof = vafc.ingest_profile()
+        profs.append({k: round(prof[k], 3) for k in ("reader_s", "main_wait_s", "submit_s", "parse_thread_s",
+                                                    "slot_wait_thread_s", "acquire_thread_s", "read_thread_s",
+                                                    "worker_cpu_s", "worker_wall_s", "threads") if k in prof})
     t2 = time.time()
     assert D.chain_holds(ranges)
     return {"scan_s": round(t1 - t0, 3), "count_s": round(t2 - t1, 3), "close_s": round(close_s, 3),
             "bases": int(bases),
-            "held": [h is not None for h in hs]}
+            "held": [h is not None for h in hs], "after_scan_mib": mem, "ingest": profs}
 
 
 def main():
@@ -94,7 +106,13 @@ def main():
         tmp = bench.scratch_dir(a.reads * 330 * 1.5, tempfile.mkdtemp(prefix="vafc_gzh_"))
         gz = os.path.join(tmp, "r.fq.gz")
         text = make_gz(gz, a.reads, a.threads)
-    out = {"gz_bytes": os.path.getsize(gz), "text_bytes": text, "world": a.world, "threads": a.threads,
+    thp = {}
+    for f in ("enabled", "defrag"):
+        try:
+            thp[f] = open("/sys/kernel/mm/transparent_hugepage/" + f).read().strip()
+        except OSError:
+            pass
+    out = {"thp": thp, "gz_bytes": os.path.getsize(gz), "text_bytes": text, "world": a.world, "threads": a.threads,
            "two_pass": [], "held": []}
     for _ in range(a.rounds):
         for key, hold in (("two_pass", 0), ("held", a.hold)):
