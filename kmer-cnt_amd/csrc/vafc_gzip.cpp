@@ -1461,13 +1461,14 @@ void VcGzParallel::sequencer()
 			if (!push_piece(std::move(P))) break;
 			continue;
 		}
+		const uint64_t nom_b = C->nom_b;   // read before the slot goes back to the workers
 		{
 			std::lock_guard<std::mutex> lk(mu_);
 			C->busy = false;
 			++stats.fallback;
 			cv_.notify_all();
 		}
-		if (!fallback(expect, C->nom_b, ended)) break;
+		if (!fallback(expect, nom_b, ended)) break;
 	}
 	// a resumed share: its last record may end in the next share, which no
 	// chunk covers -- zlib on from the share's end in small pieces (the reader
@@ -2000,8 +2001,6 @@ extern "C" uint32_t vc_gz_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t l
 {
 	return (uint32_t)crc32_combine64(crc1, crc2, (z_off64_t)len2);
 }
-
-int vc_gz_text_format(const char *path);   // vafc_ingest.cpp
 
 extern "C" void vc_gz_share_close(vc_gz_share *h)
 {
