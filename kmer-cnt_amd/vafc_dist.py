@@ -611,7 +611,10 @@ def gz_hold_budget() -> int:
     profiles/r06k_held.json); a share over the budget is inflated again."""
     env = os.environ.get("VAFC_GZ_HOLD")
     if env is not None:
-        return max(int(env), 0)
+        try:
+            return max(int(env), 0)
+        except ValueError:
+            return 0
     avail = 0
     try:
         with open("/proc/meminfo") as f:

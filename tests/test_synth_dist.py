@@ -345,3 +345,22 @@ def test_dist_driver_gzip_bad_crc_falls_back(world, manifest, synth_dir, tmp_pat
     assert all(c["restores"] >= 1 for c in calls), calls
     assert sum(c["whole"] for c in calls) == 1 and sum(c["gz_shares"] for c in calls) >= 2, calls
     assert sum(c["gz_held"] for c in calls) == (sum(c["gz_shares"] for c in calls) if world % 2 else 0)
+
+
+def test_gz_hold_budget(monkeypatch):
+    """The driver's held-share budget ($VAFC_GZ_HOLD bytes; default a quarter
+    of the available memory over the node's ranks, at most 32 GiB; a bad
+    value turns holding off rather than failing the run)."""
+    import vafc_dist as D
+    monkeypatch.setenv("VAFC_GZ_HOLD", "12345")
+    assert D.gz_hold_budget() == 12345
+    monkeypatch.setenv("VAFC_GZ_HOLD", "-1")
+    assert D.gz_hold_budget() == 0
+    monkeypatch.setenv("VAFC_GZ_HOLD", "lots")
+    assert D.gz_hold_budget() == 0
+    monkeypatch.delenv("VAFC_GZ_HOLD")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    one = D.gz_hold_budget()
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    eight = D.gz_hold_budget()
+    assert 0 < one <= 32 << 30 and eight <= one
