@@ -1166,6 +1166,7 @@ private:
 	uint64_t hold_budget_ = 0, held_bytes_ = 0;
 	bool continue_after_ = false;     // resumed share: zlib on past the last kept chunk
 	uint64_t scan_pos_ = UINT64_MAX / 2;   // held scan: the chunk the scan waits for (bounds decode-ahead)
+	uint64_t seq_first_ = UINT64_MAX;      // resumed share: the sequencer's first block (the share's start)
 	int threads_ = 1;
 
 	void worker();
@@ -1409,7 +1410,7 @@ bool VcGzParallel::fallback(uint64_t &expect, uint64_t nom_b, bool &ended, size_
 
 void VcGzParallel::sequencer()
 {
-	uint64_t expect = first_bit_;
+	uint64_t expect = seq_first_ != UINT64_MAX ? seq_first_ : first_bit_;
 	bool ended = false;
 	for (uint64_t j = 0; j < nchunks_ && !ended; ++j) {
 		Chunk *C = slots_[j % slots_.size()].get();
@@ -1585,21 +1586,21 @@ bool VcGzParallel::resume(const uint8_t *window, uint64_t text_len)
 		if (!held_) return false;
 	}
 	if (seq_.joinable()) seq_.join();
-	scan_ = false;
+	{   // workers read scan_ and may still be decoding chunks past a stream end
+		std::lock_guard<std::mutex> lk(mu_);
+		scan_ = false;
+		continue_after_ = true;
+		max_pieces_ = (size_t)threads_ + 4;
+		seq_done_ = false;
+	}
 	share_len_ = text_len;
-	continue_after_ = true;
 	if (window) {   // a later share: its history is the window before it
 		memcpy(window_.data(), window, WSIZE);
 		member_text_ = WSIZE;
 	} else {
 		member_text_ = 0;
 	}
-	first_bit_ = share_.start_bit;
-	max_pieces_ = (size_t)threads_ + 4;
-	{
-		std::lock_guard<std::mutex> lk(mu_);
-		seq_done_ = false;
-	}
+	seq_first_ = share_.start_bit;
 	const VcCpuSet cpus = vc_affinity_get();
 	seq_ = std::thread([this, cpus] {
 		vc_affinity_bind(cpus);
