@@ -1675,8 +1675,6 @@ extern "C" int vc_count_gz_share(vc_ctx *c, const char *path, int first_share, u
 	return rc;
 }
 
-int vc_gz_text_format(const char *path);   // vafc_ingest.cpp
-
 extern "C" int vc_gz_share_open(vc_ctx *c, const char *path, uint64_t begin, uint64_t end, int n_threads,
                                 uint64_t chunk_bytes, uint64_t hold_bytes, vc_gz_share_info *out,
                                 uint16_t *window_sym, vc_gz_share **held)
