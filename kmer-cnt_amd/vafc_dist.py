@@ -436,10 +436,40 @@ def count_files(files, counter, o, rank, world, err, coll_device):
     ok = True
     plan = file_plan(files, rank, world, coll_device)
     mine = [[0, 0, 0, 0] for _ in files]   # this rank's (opened, bases, seqs, microseconds) per file
-    for i, fn in enumerate(files):
+    i = -1
+    while i + 1 < len(files):
+        i += 1
+        fn = files[i]
+        kind, size = plan[i]
+        wave = _gz_wave(plan, i, world)
+        if wave:
+            # consecutive gzip files (R1.fq.gz R2.fq.gz): counted at once, each
+            # by its own group of ranks, rather than one after another by all
+            # of them -- fewer, larger shares, and none for a file that has a
+            # rank to itself
+            if rank == 0:
+                for f in wave:
+                    err("[M::main] Processing %s...\n" % files[f])
+            groups = gz_groups([plan[f][1] for f in wave], world)
+            g = next(g for g, (r0, n) in enumerate(groups) if r0 <= rank < r0 + n)
+            f = wave[g]
+            t_file = time.time()
+            res = _count_gz_group(files[f], f, plan[f][1], groups[g][0], groups[g][1], counter, o, rank, world,
+                                  err, coll_device)
+            if res is None:
+                ok = False
+                break
+            good, b, s, fell, local_ok = res
+            fallbacks += fell
+            ok = ok and local_ok
+            bases += b
+            seqs += s
+            if good:
+                mine[f] = [1, b, s, int(1e6 * (time.time() - t_file))]
+            i = wave[-1]
+            continue
         if rank == 0:
             err("[M::main] Processing %s...\n" % fn)
-        kind, size = plan[i]
         t_file = time.time()
         if kind == 2:
             res = _count_gz_shares(fn, i, size, counter, o, rank, world, err, coll_device)
@@ -519,88 +549,145 @@ def count_files(files, counter, o, rank, world, err, coll_device):
     return ok, bases, seqs, fallbacks, per_file
 
 
+def _gz_wave(plan, i, world):
+    """The files counted together from file i on (count_files): the run of
+    consecutive gzip files (kind 2) starting there, at most one per rank;
+    empty unless it holds two or more."""
+    wave = []
+    while i < len(plan) and plan[i][0] == 2 and len(wave) < world:
+        wave.append(i)
+        i += 1
+    return wave if len(wave) >= 2 else []
+
+
 def _count_gz_shares(fn, i, size, counter, o, rank, world, err, coll_device):
-    """File i, a gzip file, over the ranks (include/vafc.h, vafc_gzip.h):
-    every rank scans its share of the stream, the shares' windows follow from
-    one all-gather, every rank counts its share, and the ranges and CRC-32
-    accounting are checked as one chain.  Anything that does not chain (a
-    share that cannot be decoded blind, a record split wrongly, a member that
-    fails its check) is counted whole by rank i mod N instead, which is
-    exactly vc_count_file.  Returns (opened, bases, seqs, fallbacks, ok) of
-    this rank (ok False: its whole-file count failed; the other ranks go on, as
-    for a file dealt whole), or None when a rank failed during the shares (all
-    ranks stop)."""
+    """File i, a gzip file, over all the ranks: _count_gz_group with one group."""
+    return _count_gz_group(fn, i, size, 0, world, counter, o, rank, world, err, coll_device)
+
+
+def gz_groups(sizes, world: int):
+    """Ranks per file for a wave of len(sizes) <= world gzip files counted at
+    once (count_files): at least one rank each, the rest shared out by
+    compressed size (largest remainder, ties to the earlier file); returns
+    [(first rank, ranks)] in file order, covering ranks 0 .. world-1."""
+    g = len(sizes)
+    assert 1 <= g <= world
+    w = [max(int(x), 1) for x in sizes]
+    spare = world - g
+    want = [spare * x / sum(w) for x in w]
+    extra = [int(x) for x in want]
+    for f in sorted(range(g), key=lambda f: (extra[f] - want[f], f))[:spare - sum(extra)]:
+        extra[f] += 1
+    out, r = [], 0
+    for f in range(g):
+        out.append((r, 1 + extra[f]))
+        r += 1 + extra[f]
+    return out
+
+
+def _count_gz_group(fn, i, size, first, n, counter, o, rank, world, err, coll_device):
+    """File i, a gzip file, over ranks first .. first+n-1 (include/vafc.h,
+    vafc_gzip.h); the other ranks count other files of the same wave at the
+    same time, and every rank takes part in the same three all-gathers.  One
+    rank: the file whole.  Several: each scans its share of the stream, the
+    shares' windows follow from the scans' symbols, each counts its share, and
+    the ranges and CRC-32 accounting are checked as one chain.  Anything that
+    does not chain (a share that cannot be decoded blind, a record split
+    wrongly, a member that fails its check) is counted whole by rank
+    first + i mod n instead, which is exactly vc_count_file.  Returns (opened,
+    bases, seqs, fallbacks, ok) of this rank (ok False: its whole-file count
+    failed; the other ranks go on, as for a file dealt whole), or None when a
+    rank failed during the shares (all ranks stop)."""
     import vafc
-    begin, end = byte_range(size, rank, world)
+    me = rank - first
+    assert 0 <= me < n
     failed = False
     info = {"start_bit": NO_OFFSET, "end_bit": NO_OFFSET, "text_len": 0, "ok": 1, "ended": 0}
     wsym = np.zeros(vafc.GZ_WSIZE, np.uint16)
     hold = int(counter.gz_hold_bytes)
     share = None
+    if n > 1:
+        begin, end = byte_range(size, me, n)
+        try:
+            if end > begin and hold > 0:     # one inflate pass: the scan's chunks kept for the count
+                info, wsym, share = vafc.gz_share_open(fn, begin, end, threads=o["t"], hold_bytes=hold,
+                                                       kmap=counter.gz_kmap())
+            elif end > begin:
+                info, wsym = vafc.gz_share_scan(fn, begin, end, threads=o["t"])
+        except FileNotFoundError:
+            info["ok"] = 0
+        except Exception as e:
+            err("Error: counting failed on %s (%s)\n" % (fn, e))
+            failed = True
     try:
-        if end > begin and hold > 0:     # one inflate pass: the scan's chunks kept for the count
-            info, wsym, share = vafc.gz_share_open(fn, begin, end, threads=o["t"], hold_bytes=hold,
-                                                   kmap=counter.gz_kmap())
-        elif end > begin:
-            info, wsym = vafc.gz_share_scan(fn, begin, end, threads=o["t"])
-    except FileNotFoundError:
-        info["ok"] = 0
-    except Exception as e:
-        err("Error: counting failed on %s (%s)\n" % (fn, e))
-        failed = True
-    try:
-        return _count_gz_share_scanned(fn, i, counter, o, rank, world, err, coll_device, info, wsym, share, failed)
+        return _count_gz_group_scanned(fn, i, first, n, counter, o, rank, world, err, coll_device, info, wsym,
+                                       share, failed)
     finally:
         if share is not None:
             share.close()
 
 
-def _count_gz_share_scanned(fn, i, counter, o, rank, world, err, coll_device, info, wsym, share, failed):
-    """_count_gz_shares after this rank's scan (share: its held chunks, or None)."""
+def _count_gz_group_scanned(fn, i, first, n, counter, o, rank, world, err, coll_device, info, wsym, share, failed):
+    """_count_gz_group after this rank's scan (share: its held chunks, or None)."""
     import vafc
+    me = rank - first
+    leader = first + i % n
     rows = allgather_ints([info["start_bit"], info["end_bit"], info["text_len"], info["ok"], info["ended"],
                            1 if failed else 0], world, coll_device)
     if any(r[5] for r in rows):
         return None
     wsyms = allgather_u16(wsym, world, coll_device)
+    grows = rows[first:first + n]
 
     def whole():
-        if i % world != rank:
-            return False, 0, 0, 1, True
+        """(good, bases, seqs, ok) of the whole-file count on this rank."""
         try:
             good, b, s, _ = counter.count_range(fn, 0, NO_OFFSET, o["b"], o["t"])
         except Exception as e:
             err("Error: counting failed on %s (%s)\n" % (fn, e))
-            return False, 0, 0, 1, False
-        return (True, b, s, 1, True) if good else (False, 0, 0, 1, True)
+            return False, 0, 0, False
+        return (good, b, s, True) if good else (False, 0, 0, True)
 
-    if not gz_shares_chain(rows):
-        return whole()
-    windows = gz_windows(rows, wsyms)
-    counter.save()
-    good, b, s, rinfo, crc = True, 0, 0, (EMPTY_RANGE, EMPTY_RANGE, 0, 0), None
-    if int(rows[rank][0]) != NO_OFFSET:
-        try:
-            if share is not None:
-                good, b, s, rinfo, crc = counter.count_gz_share_held(share, rank == 0, windows[rank],
-                                                                     int(rows[rank][2]), o["b"], o["t"])
-            else:
-                good, b, s, rinfo, crc = counter.count_gz_share(fn, rank == 0, int(rows[rank][0]), windows[rank],
-                                                                int(rows[rank][2]), o["b"], o["t"])
-        except Exception as e:
-            err("Error: counting failed on %s (%s)\n" % (fn, e))
-            failed = True
+    # the count: the file whole (one rank, or shares that do not chain: the
+    # leader alone), else this rank's share
+    split = n > 1 and gz_shares_chain(grows)
+    good, b, s, rinfo, crc, local_ok = False, 0, 0, (EMPTY_RANGE, EMPTY_RANGE, 0, 0), None, True
+    if not split:
+        if rank == leader:
+            good, b, s, local_ok = whole()
+            failed = failed or (n == 1 and not local_ok)   # a lone rank's failure stops the wave
+    else:
+        windows = gz_windows(grows, wsyms[first:first + n])
+        counter.save()
+        good = True
+        if int(grows[me][0]) != NO_OFFSET:
+            try:
+                if share is not None:
+                    good, b, s, rinfo, crc = counter.count_gz_share_held(share, me == 0, windows[me],
+                                                                         int(grows[me][2]), o["b"], o["t"])
+                else:
+                    good, b, s, rinfo, crc = counter.count_gz_share(fn, me == 0, int(grows[me][0]), windows[me],
+                                                                    int(grows[me][2]), o["b"], o["t"])
+            except Exception as e:
+                err("Error: counting failed on %s (%s)\n" % (fn, e))
+                failed = True
     cvals = [int((crc or {}).get(f, 0)) for f in GZ_CRC_FIELDS]
     res = allgather_ints(list(rinfo) + [1 if good else 0, 1 if failed else 0] + cvals, world, coll_device)
     if any(r[5] for r in res):
         return None
-    nonempty = [r for r in range(world) if int(rows[r][0]) != NO_OFFSET]
-    crcs = [dict(zip(GZ_CRC_FIELDS, (int(x) for x in res[r][6:]))) for r in nonempty]
-    if all(res[r][4] for r in nonempty) and chain_holds([res[r][:4] for r in range(world)]) and \
+    if not split:
+        return (good, b, s, 0 if n == 1 else 1, local_ok) if rank == leader else (False, 0, 0, 1, True)
+    gres = res[first:first + n]
+    nonempty = [r for r in range(n) if int(grows[r][0]) != NO_OFFSET]
+    crcs = [dict(zip(GZ_CRC_FIELDS, (int(x) for x in gres[r][6:]))) for r in nonempty]
+    if all(gres[r][4] for r in nonempty) and chain_holds([gres[r][:4] for r in range(n)]) and \
             gz_crc_chain(crcs, vafc.gz_crc32_combine):
         return good, b, s, 0, True
     counter.restore()
-    return whole()
+    if rank != leader:
+        return False, 0, 0, 1, True
+    good, b, s, local_ok = whole()
+    return good, b, s, 1, local_ok
 
 
 def gz_hold_budget() -> int:

@@ -39,7 +39,10 @@ def main():
     manifest["cases"] = [c for c in manifest["cases"] if not c["name"].startswith("gz_")]
     for name, files in (("gz_multi_k21", ["c1_10k_multi.fq.gz"]),
                         ("gz_trailing_k21", ["c1_10k_trailing.fq.gz"]),
-                        ("gz_mixed_k21", ["c1_10k_multi.fq.gz", "c1_10k.fq", "c1_10k_trailing.fq.gz"])):
+                        ("gz_mixed_k21", ["c1_10k_multi.fq.gz", "c1_10k.fq", "c1_10k_trailing.fq.gz"]),
+                        # consecutive gzip files: one wave of rank groups in vafc_dist (round 6)
+                        ("gz_pair_k21", ["c1_10k_multi.fq.gz", "c1_10k_trailing.fq.gz"]),
+                        ("gz_trio_k21", ["c1_10k_trailing.fq.gz", "c1_10k_multi.fq.gz", "c1_10k_trailing.fq.gz"])):
         argv = ["-v", "-k", "21", "-t", "2", "-p", "grch38_k21.txt"] + files
         rc, stats, err = G.run_ref(argv + ["-o", "out.vaf"], d)
         out = os.path.join(d, "out.vaf")

@@ -143,6 +143,8 @@ DIST_CASES = ["pe_k31", "c1_plumbing_k21", "c1_plumbing_k21_gz", "c1_k21_b1", "m
 DIST_CLEAN = {"pe_k31", "c1_plumbing_k21", "c1_k21_b1", "pal_k16"}
 # well-formed gzip (and plain) files: shares of the stream, no whole-file count
 DIST_GZ_CLEAN = {"c1_plumbing_k21_gz", "edge_gz", "gz_multi_k21", "gz_trailing_k21", "gz_mixed_k21"}
+# consecutive gzip files: counted a wave at a time, each file by its own group of ranks
+DIST_GZ_WAVES = {"gz_pair_k21", "gz_trio_k21"}
 
 
 def _driver_rank(rank, world, port, argv, cwd, out_json, counter):
@@ -274,7 +276,10 @@ def _run_driver(entry, synth_dir, tmp_path, counter, world=2):
 @pytest.mark.parametrize("name,world", [(n, 2) for n in DIST_CASES] + [("c1_plumbing_k21", 3), ("pe_k31", 3),
                                                                        ("mal_bg", 3), ("c1_plumbing_k21_gz", 3),
                                                                        ("gz_multi_k21", 3), ("gz_multi_k21", 5),
-                                                                       ("edge_gz", 3), ("gz_mixed_k21", 3)])
+                                                                       ("edge_gz", 3), ("gz_mixed_k21", 3),
+                                                                       ("gz_pair_k21", 2), ("gz_pair_k21", 3),
+                                                                       ("gz_pair_k21", 5), ("gz_trio_k21", 2),
+                                                                       ("gz_trio_k21", 4)])
 def test_dist_driver_matches_reference(name, world, counter, manifest, synth_dir, tmp_path):
     """vafc_dist.run over gloo ranks (the oracle as the per-rank counter on
     CPU; the HIP counter, every rank on device 0, in the GPU suite): plain
@@ -315,6 +320,22 @@ def test_dist_driver_matches_reference(name, world, counter, manifest, synth_dir
             assert sum(c["gz_held"] for c in calls) == (sum(c["gz_shares"] for c in calls) if world % 2 else 0)
         if name.startswith("mal_") or name == "truncated":
             assert all(c["restores"] >= 1 for c in calls), calls
+        if name in DIST_GZ_WAVES:   # a lone rank counts its file whole, a group splits it into shares
+            import vafc_dist as D
+            plan = [(2, os.path.getsize(os.path.join(case_dir(entry, synth_dir), f))) for f in inputs]
+            whole, split, most = 0, 0, 0
+            i = 0
+            while i < len(plan):
+                wave = D._gz_wave(plan, i, world) or [i]
+                groups = D.gz_groups([plan[f][1] for f in wave], world) if len(wave) > 1 else [(0, world)]
+                for _, n in groups:
+                    whole += n == 1
+                    split += n > 1
+                    most += n if n > 1 else 0
+                i = wave[-1] + 1
+            assert all(c["restores"] == 0 for c in calls), calls
+            assert sum(c["whole"] for c in calls) == whole, calls
+            assert split <= sum(c["gz_shares"] for c in calls) <= most, calls
 
 
 def test_dist_driver_usage_and_missing_patterns(tmp_path):
@@ -364,3 +385,20 @@ def test_gz_hold_budget(monkeypatch):
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
     eight = D.gz_hold_budget()
     assert 0 < one <= 32 << 30 and eight <= one
+
+
+def test_dist_driver_gzip_wave_bad_crc_falls_back(manifest, synth_dir, tmp_path):
+    """A wave of two gzip files over three ranks, the first with a middle
+    member that fails its CRC-32 check: its group of ranks counts shares, the
+    combined check fails and its leader counts it whole, while the other
+    file's group is not disturbed -- the same .vaf as the single-rank driver."""
+    entry = {"name": "gz_wave_badcrc", "argv": ["-v", "-k", "21", "-t", "2", "-p", "grch38_k21.txt",
+                                                "c1_10k_badcrc.fq.gz", "c1_10k_multi.fq.gz"],
+             "inputs": ["synth:grch38_k21.txt", "synth:c1_10k_badcrc.fq.gz", "synth:c1_10k_multi.fq.gz"]}
+    (tmp_path / "w1").mkdir()
+    rcs1, stats1, data1, _, _ = _run_driver(entry, synth_dir, tmp_path / "w1", "oracle", 1)
+    rcs, stats, data, err, calls = _run_driver(entry, synth_dir, tmp_path, "oracle", 3)
+    assert rcs == [0] * 3 and rcs1 == [0], err[-2000:]
+    assert data == data1 and stats == stats1
+    assert sum(c["restores"] for c in calls) >= 1, calls
+    assert sum(c["whole"] for c in calls) == 2, calls   # the bad file's recount, the other file's lone rank
