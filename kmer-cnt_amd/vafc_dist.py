@@ -552,7 +552,9 @@ def count_files(files, counter, o, rank, world, err, coll_device):
 def _gz_wave(plan, i, world):
     """The files counted together from file i on (count_files): the run of
     consecutive gzip files (kind 2) starting there, at most one per rank;
-    empty unless it holds two or more."""
+    empty unless it holds two or more ($VAFC_GZ_WAVES=0: never, A/B)."""
+    if os.environ.get("VAFC_GZ_WAVES") == "0":
+        return []
     wave = []
     while i < len(plan) and plan[i][0] == 2 and len(wave) < world:
         wave.append(i)

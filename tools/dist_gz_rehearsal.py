@@ -26,11 +26,13 @@ sys.path.insert(0, os.path.join(ROOT, "kmer-cnt_amd"))
 DRIVER = os.path.join(ROOT, "kmer-cnt_amd", "vafc_dist.py")
 
 
-def run(n, threads, pat, gz, out, timeout=600, hold=None):
+def run(n, threads, pat, gzs, out, timeout=600, hold=None, waves=True):
     env = dict(os.environ, VAFC_DIST_BACKEND="gloo", VAFC_REHEARSAL="1")
     if hold is not None:
         env["VAFC_GZ_HOLD"] = str(hold)
-    argv = ["-v", "-k", "21", "-t", str(threads), "-p", pat, "-o", out, gz]
+    if not waves:
+        env["VAFC_GZ_WAVES"] = "0"
+    argv = ["-v", "-k", "21", "-t", str(threads), "-p", pat, "-o", out] + list(gzs)
     t0 = time.time()
     if n == 1:
         env.pop("WORLD_SIZE", None)
@@ -66,6 +68,7 @@ def main():
     ap.add_argument("--ranks", type=int, default=2)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--threads", type=int, default=16, help="reader threads of the box (split over the ranks)")
+    ap.add_argument("--files", type=int, default=1, help="the reads as this many gzip files (R1, R2, ...)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -87,31 +90,38 @@ def main():
                      win.data_ptr(), dos.data_ptr(), panel.n, 0)
     torch.cuda.synchronize()
     work = bench.scratch_dir(R * (2 * L + 16) * 1.5, tmp)
-    fq = os.path.join(work, "c2.fq")
-    bench.write_fastq_from_device(d_seq, R, L, fq, threads=a.threads)
+    gzs, gz_bytes, text = [], 0, 0
+    per = R // a.files
+    for f in range(a.files):
+        fq = os.path.join(work, "c2_%d.fq" % f)
+        n = per if f + 1 < a.files else R - per * f
+        bench.write_fastq_from_device(d_seq[f * per * L:], n, L, fq, threads=a.threads, first=f * per)
+        gzs.append(fq + ".gz")
+        gz_bytes += bench.gzip_level1(fq, gzs[-1], a.threads)
+        text += os.path.getsize(fq)
+        os.unlink(fq)
     del d_seq, d_offs, d_lens
     torch.cuda.empty_cache()
-    gz = fq + ".gz"
-    gz_bytes = bench.gzip_level1(fq, gz, a.threads)
-    text = os.path.getsize(fq)
-    os.unlink(fq)
     sys.stderr.write("[gzr] %d reads, %.2f GB of text, %.2f GB gzip\n" % (R, text / 1e9, gz_bytes / 1e9))
-    out = {"workload": "%dM x %d bp reads of the C2 stream as one pigz-shaped level-1 gzip FASTQ (%.2f GB, %.2f GB "
-                       "of text) in the page cache; k = 21, the GRCh38 panel" % (R // 10**6, L, gz_bytes / 1e9,
-                                                                                text / 1e9),
+    out = {"workload": "%dM x %d bp reads of the C2 stream as %d pigz-shaped level-1 gzip FASTQ file(s) (%.2f GB, "
+                       "%.2f GB of text) in the page cache; k = 21, the GRCh38 panel" % (R // 10**6, L, a.files,
+                                                                                        gz_bytes / 1e9, text / 1e9),
            "box": "one GPU box, %d reader threads in all: 1 rank x %d against %d ranks x %d (gloo, every rank on "
                   "GPU 0)" % (a.threads, a.threads, a.ranks, max(1, a.threads // a.ranks)),
            "runs": {"1": [], str(a.ranks): [], "%d_two_pass" % a.ranks: []}}
+    legs = [(1, None, True, "1"), (a.ranks, None, True, str(a.ranks)), (a.ranks, 0, True, "%d_two_pass" % a.ranks)]
+    if a.files > 1:   # the files one after another, each split over every rank
+        legs.append((a.ranks, None, False, "%d_no_waves" % a.ranks))
+        out["runs"]["%d_no_waves" % a.ranks] = []
     md5s = {}
-    run(1, a.threads, pat, gz, os.path.join(tmp, "warm.vaf"))
+    run(1, a.threads, pat, gzs, os.path.join(tmp, "warm.vaf"))
     for rep in range(a.rounds):
         # N ranks with the scans' chunks held for the count (one inflate pass,
         # the driver's default budget) and with holding off (VAFC_GZ_HOLD=0:
         # every share inflated twice)
-        for n, hold, key in ((1, None, "1"), (a.ranks, None, str(a.ranks)),
-                             (a.ranks, 0, "%d_two_pass" % a.ranks)):
+        for n, hold, waves, key in legs:
             o = os.path.join(tmp, "r%s.vaf" % key)
-            r = run(n, max(1, a.threads // n), pat, gz, o, hold=hold)
+            r = run(n, max(1, a.threads // n), pat, gzs, o, hold=hold, waves=waves)
             md5s[key] = bench.md5(o)
             out["runs"][key].append(r)
             sys.stderr.write("[gzr] %s rank(s), round %d: %.1f Mbases/s\n" % (key, rep + 1, r["mbases"]))
@@ -120,7 +130,8 @@ def main():
                    "share is inflated once; two_pass: the scan's output is dropped and the count inflates the "
                    "share again from its start bit with the known window")
     print(json.dumps(out))
-    os.unlink(gz)
+    for gz in gzs:
+        os.unlink(gz)
     if work != tmp:
         shutil.rmtree(work, ignore_errors=True)
     shutil.rmtree(tmp, ignore_errors=True)
