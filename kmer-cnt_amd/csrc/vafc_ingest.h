@@ -151,10 +151,13 @@ int vc_ingest_plain(int fd, uint64_t size, int k, int block_bases, int threads, 
 class VcGzParallel;
 // Parse workers for gzip input inflated by `threads` workers: the inflate
 // is several times slower per byte than the parse ($VAFC_GZ_PARSERS overrides).
+// One in four: at -t 16 the CLI's gzip pass ran 5.07-5.14 Gbases/s with 4
+// parsers against 4.36-4.52 with 3 and 4.97-5.04 with 5 once the inflater's
+// buffers stopped regrowing (profiles/r06u_gz_sweep.log; one in five before).
 inline int vc_gz_parse_threads(int threads)
 {
 	const char *e = getenv("VAFC_GZ_PARSERS");
-	const int n = e && atoi(e) > 0 ? atoi(e) : (threads + 3) / 5;
+	const int n = e && atoi(e) > 0 ? atoi(e) : (threads + 2) / 4;
 	return n < 1 ? 1 : n;
 }
 // Parse workers for a held gzip share (vc_count_gz_share_held): its chunks
