@@ -6,22 +6,12 @@
 // on the GPU (device: $VAFC_DEVICE, default 0), or on several: $VAFC_DEVICES
 // is a comma-separated device list, one shard per entry (vc_create_multi:
 // batches dealt round robin, one RCCL reduce before the .vaf is written).
-//
-// Two consecutive gzip inputs (R1.fq.gz R2.fq.gz) on one device are counted
-// at the same time, each by half of the -t threads into a counter of its own
-// (the counts are sums, so the order does not matter; the two are added
-// before the .vaf is written): one inflater over 16 threads scales worse than
-// two over 8.  The messages keep the reference's order:
-// "Processing" of the second file is printed after the first one's
-// "Processed" line.  VAFC_GZ_PAIRS=0 counts them one after the other.
 #include <getopt.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
-#include <sys/stat.h>
 #include <time.h>
 
-#include <thread>
 #include <vector>
 
 #include "vafc.h"
@@ -31,19 +21,6 @@ static double now_s()
 	struct timespec ts;
 	clock_gettime(CLOCK_REALTIME, &ts);
 	return ts.tv_sec + ts.tv_nsec * 1e-9;
-}
-
-// A regular file that starts with the gzip magic bytes.
-static bool is_gzip(const char *path)
-{
-	struct stat sb;
-	if (stat(path, &sb) != 0 || !S_ISREG(sb.st_mode)) return false;
-	FILE *f = fopen(path, "rb");
-	if (!f) return false;
-	unsigned char m[2];
-	const bool g = fread(m, 1, 2, f) == 2 && m[0] == 0x1f && m[1] == 0x8b;
-	fclose(f);
-	return g;
 }
 
 static void usage(int k, int n_thread, int block)
@@ -126,26 +103,12 @@ int main(int argc, char *argv[])
 		        "Some patterns may have overlapping k-mers.\n", "create_combined_kmer_map", n_coll);
 	vc_ctx *ctx = nullptr;
 	rc = vc_create_multi(&ctx, k, keys, vals, n_keys, (uint32_t)n, devices.data(), (int)devices.size());
-	// a second counter for pairs of consecutive gzip inputs (see the top)
-	std::vector<char> gz(argc, 0);
-	bool pairs = false;
-	if (devices.size() == 1 && n_thread >= 4 && !(getenv("VAFC_GZ_PAIRS") && !strcmp(getenv("VAFC_GZ_PAIRS"), "0"))) {
-		for (int i = optind; i < argc; ++i) gz[i] = is_gzip(argv[i]);
-		for (int i = optind; i + 1 < argc; ++i) pairs = pairs || (gz[i] && gz[i + 1]);
-	}
-	vc_ctx *ctx2 = nullptr;
-	if (rc == VC_OK && pairs)
-		rc = vc_create_multi(&ctx2, k, keys, vals, n_keys, (uint32_t)n, devices.data(), (int)devices.size());
 	vc_free(keys);
 	vc_free(vals);
-	auto cleanup = [&]() {
-		vc_destroy(ctx2);
-		vc_destroy(ctx);
-		vc_patterns_free(db);
-	};
 	if (rc != VC_OK) {
 		fprintf(stderr, "Error: failed to create k-mer map (%s)\n", vc_strerror(rc));
-		cleanup();
+		vc_destroy(ctx);
+		vc_patterns_free(db);
 		return 1;
 	}
 	const double t_map = now_s() - t;
@@ -164,64 +127,33 @@ int main(int argc, char *argv[])
 	const double t_reserved = now_s();
 	if (rc != VC_OK) {
 		fprintf(stderr, "Error: counting failed (%s)\n", vc_strerror(rc));
-		cleanup();
+		vc_destroy(ctx);
+		vc_patterns_free(db);
 		return 1;
 	}
 	uint64_t tot_bases = 0, tot_seqs = 0;
-	// a file's outcome as the reference reports it; false: exit 1
-	auto done = [&](const char *fn, int frc, const vc_file_stats &st) {
-		if (frc == VC_EIO) return true;   // unopenable input is skipped silently (vaf-counter.c:557)
-		if (frc != VC_OK) {
-			fprintf(stderr, "Error: counting failed on %s (%s)\n", fn, vc_strerror(frc));
-			return false;
+	for (int i = optind; i < argc; ++i) {
+		fprintf(stderr, "[M::%s] Processing %s...\n", "main", argv[i]);
+		vc_file_stats st;
+		rc = vc_count_file(ctx, argv[i], block, n_thread, &st);
+		if (rc == VC_EIO) continue;   // unopenable input is skipped silently (vaf-counter.c:557)
+		if (rc != VC_OK) {
+			fprintf(stderr, "Error: counting failed on %s (%s)\n", argv[i], vc_strerror(rc));
+			vc_destroy(ctx);
+			vc_patterns_free(db);
+			return 1;
 		}
 		tot_bases += st.bases;
 		tot_seqs += st.seqs;
 		if (verbose)
 			fprintf(stderr, "[V::%s] Processed %s: %llu sequences, %llu bases in %.2f sec (%.2f Mbases/sec)\n",
-			        "count_fastq_kmers", fn, (unsigned long long)st.seqs, (unsigned long long)st.bases, st.seconds,
-			        st.bases / st.seconds / 1e6);
-		return true;
-	};
-	bool used2 = false;
-	for (int i = optind; i < argc; ++i) {
-		fprintf(stderr, "[M::%s] Processing %s...\n", "main", argv[i]);
-		vc_file_stats st = {0, 0, 0, 0.0}, st2 = {0, 0, 0, 0.0};
-		if (!(ctx2 && i + 1 < argc && gz[i] && gz[i + 1])) {
-			if (!done(argv[i], vc_count_file(ctx, argv[i], block, n_thread, &st), st)) {
-				cleanup();
-				return 1;
-			}
-			continue;
-		}
-		const int t1 = n_thread / 2;
-		int rc2 = VC_OK;
-		std::thread second([&]() { rc2 = vc_count_file(ctx2, argv[i + 1], block, n_thread - t1, &st2); });
-		const int rc1 = vc_count_file(ctx, argv[i], block, t1, &st);
-		second.join();
-		used2 = true;
-		if (!done(argv[i], rc1, st)) {
-			cleanup();
-			return 1;
-		}
-		++i;
-		fprintf(stderr, "[M::%s] Processing %s...\n", "main", argv[i]);
-		if (!done(argv[i], rc2, st2)) {
-			cleanup();
-			return 1;
-		}
+			        "count_fastq_kmers", argv[i], (unsigned long long)st.seqs,
+			        (unsigned long long)st.bases, st.seconds, st.bases / st.seconds / 1e6);
 	}
 	std::vector<uint32_t> counts(2 * (size_t)n + 2, 0);
 	uint64_t kmers = 0;
 	const double t_read = now_s();
 	rc = vc_finish(ctx, counts.data(), &kmers);
-	if (rc == VC_OK && used2) {   // the second counter's counts added (u32 sums wrap as the reference's do)
-		std::vector<uint32_t> counts2(counts.size(), 0);
-		uint64_t kmers2 = 0;
-		rc = vc_finish(ctx2, counts2.data(), &kmers2);
-		for (size_t j = 0; j < counts.size(); ++j) counts[j] += counts2[j];
-		kmers += kmers2;
-	}
 	const double t_count = now_s() - t;
 	// VAFC_PHASES=1: the counting timer split into the reader's buffer
 	// allocation (pinned slots of every shard), the reading and counting of
@@ -233,7 +165,8 @@ int main(int argc, char *argv[])
 		        now_s() - t_read, t_count);
 	if (rc != VC_OK) {
 		fprintf(stderr, "Error: counting failed (%s)\n", vc_strerror(rc));
-		cleanup();
+		vc_destroy(ctx);
+		vc_patterns_free(db);
 		return 1;
 	}
 	uint64_t tot_ref = 0, tot_alt = 0;
@@ -247,7 +180,8 @@ int main(int argc, char *argv[])
 	t = now_s();
 	if (vc_write_vaf(db, counts.data(), out_fn) != VC_OK) {
 		fprintf(stderr, "Error: failed to open output file\n");
-		cleanup();
+		vc_destroy(ctx);
+		vc_patterns_free(db);
 		return 1;
 	}
 	const double t_write = now_s() - t;
@@ -288,6 +222,7 @@ int main(int argc, char *argv[])
 		fprintf(stderr, "  Threads:               %d workers\n", n_thread);
 		fprintf(stderr, "==============================\n");
 	}
-	cleanup();
+	vc_destroy(ctx);
+	vc_patterns_free(db);
 	return 0;
 }

@@ -99,28 +99,6 @@ def test_cli_matches_reference(name, manifest, synth_dir, tmp_path):
     assert ("collisions detected" in err) == entry["collision_warning"]
 
 
-@pytest.mark.parametrize("name", ["gz_pair_k21", "gz_trio_k21", "gz_mixed_k21"])
-@pytest.mark.parametrize("pairs", ["1", "0"])
-def test_cli_gzip_pairs_match_reference(name, pairs, manifest, synth_dir, tmp_path):
-    """Consecutive gzip inputs at -t 8: the CLI counts a pair of them at the
-    same time into two counters (vaf_counter_main.cpp; VAFC_GZ_PAIRS=0 one
-    after the other).  The .vaf and tallies are the reference's either way,
-    and the messages keep its order: Processing / Processed per file."""
-    entry = dict(next(c for c in manifest["cases"] if c["name"] == name))
-    argv = list(entry["argv"])
-    argv[argv.index("-t") + 1] = "8"
-    entry["argv"] = argv
-    rc, stats, data, err = run_cli(PRODUCT_CLI, entry, synth_dir, tmp_path, env=dict(os.environ, VAFC_GZ_PAIRS=pairs))
-    assert rc == 0, err[-2000:]
-    assert hashlib.md5(data).hexdigest() == entry["vaf_md5"]
-    for key in ("bases", "seqs", "kmers"):
-        assert stats.get(key) == entry["stats"].get(key), key
-    inputs = [a for a in argv if a.endswith((".fq", ".gz"))]
-    seq = [ln.split("] ")[1].split(" ")[0] + " " + ln.split(" ")[2].rstrip(".:")
-           for ln in err.splitlines() if "] Processing " in ln or "] Processed " in ln]
-    assert seq == [w for f in inputs for w in ("Processing " + f, "Processed " + f)], seq
-
-
 @pytest.mark.parametrize("name", ["c1_plumbing_k21", "pe_k31", "edge_k15", "mal_gbbbg_b1"])
 def test_python_mirror_matches_reference(name, manifest, synth_dir, tmp_path):
     import vafc

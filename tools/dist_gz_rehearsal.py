@@ -69,9 +69,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--threads", type=int, default=16, help="reader threads of the box (split over the ranks)")
     ap.add_argument("--files", type=int, default=1, help="the reads as this many gzip files (R1, R2, ...)")
-    ap.add_argument("--cli", action="store_true", help="also the drop-in CLI over the files, with its gzip pairs "
-                                                       "counted at once and one after the other (VAFC_GZ_PAIRS)")
-    ap.add_argument("--no-driver", action="store_true", help="skip the torchrun-style driver legs")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -117,20 +114,8 @@ def main():
         legs.append((a.ranks, None, False, "%d_no_waves" % a.ranks))
         out["runs"]["%d_no_waves" % a.ranks] = []
     md5s = {}
-    if a.cli:
-        out["cli"] = {"pairs": [], "sequential": []}
-        for rep in range(a.rounds):
-            for key, v in (("pairs", "1"), ("sequential", "0")):
-                o = os.path.join(tmp, "cli_%s.vaf" % key)
-                r = bench.cli_run(bench.PRODUCT_CLI, pat, gzs, a.threads, o, 21, env=dict(os.environ, VAFC_GZ_PAIRS=v))
-                md5s["cli_" + key] = bench.md5(o)
-                out["cli"][key].append({"mbases": r["mbases"], "wall": round(r["wall"], 2)})
-                sys.stderr.write("[gzr] CLI %s, round %d: %.1f Mbases/s\n" % (key, rep + 1, r["mbases"]))
-    if a.no_driver:
-        legs = []
-    else:
-        run(1, a.threads, pat, gzs, os.path.join(tmp, "warm.vaf"))
-    for rep in range(a.rounds if legs else 0):
+    run(1, a.threads, pat, gzs, os.path.join(tmp, "warm.vaf"))
+    for rep in range(a.rounds):
         # N ranks with the scans' chunks held for the count (one inflate pass,
         # the driver's default budget) and with holding off (VAFC_GZ_HOLD=0:
         # every share inflated twice)
