@@ -402,3 +402,22 @@ def test_dist_driver_gzip_wave_bad_crc_falls_back(manifest, synth_dir, tmp_path)
     assert data == data1 and stats == stats1
     assert sum(c["restores"] for c in calls) >= 1, calls
     assert sum(c["whole"] for c in calls) == 2, calls   # the bad file's recount, the other file's lone rank
+
+
+def test_gz_groups_cover_the_ranks():
+    """gz_groups: every rank in exactly one group, in file order, each file at
+    least one rank, the spare ranks shared by compressed size; _gz_wave: runs
+    of consecutive gzip files, at most one per rank, two or more."""
+    import vafc_dist as D
+    for sizes in ([1, 1], [10, 30], [5, 5, 5], [100, 1], [0, 0, 0], [7, 3, 9, 1]):
+        for world in range(len(sizes), 10):
+            g = D.gz_groups(sizes, world)
+            assert [r0 for r0, _ in g] == [sum(n for _, n in g[:f]) for f in range(len(sizes))]
+            assert sum(n for _, n in g) == world and all(n >= 1 for _, n in g)
+            big, small = max(range(len(sizes)), key=lambda f: sizes[f]), min(range(len(sizes)), key=lambda f: sizes[f])
+            assert g[big][1] >= g[small][1]
+    plan = [(2, 5), (2, 5), (1, 9), (2, 5), (2, 5), (2, 5), (0, -1)]
+    assert D._gz_wave(plan, 0, 4) == [0, 1]
+    assert D._gz_wave(plan, 2, 4) == []
+    assert D._gz_wave(plan, 3, 2) == [3, 4] and D._gz_wave(plan, 5, 2) == []
+    assert D._gz_wave(plan, 0, 1) == []
